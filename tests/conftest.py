@@ -1,0 +1,29 @@
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+TESTS = os.path.dirname(os.path.abspath(__file__))
+if TESTS not in sys.path:
+    sys.path.insert(0, TESTS)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path through the C ABI)")
+    config.addinivalue_line("markers", "slow: long-running parity case")
+
+
+@pytest.fixture(scope="session")
+def golden():
+    import json
+
+    d = os.path.join(TESTS, "golden")
+
+    def load(name):
+        with open(os.path.join(d, name)) as f:
+            return json.load(f)
+
+    return load
