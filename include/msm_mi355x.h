@@ -1,0 +1,111 @@
+/*
+ * msm_mi355x.h -- C ABI of the MI355X (gfx950) BLS12-381 MSM engine
+ * (libmsm_mi355x.so, built from msm_blst_amd/csrc).
+ *
+ * Drop-in boundary for the hot path of LuoGuiwen/MSM_blst (a blst v0.3.10
+ * fork): plain C types and pointers only, layout-identical to
+ * bindings/blst.h, so a caller of the reference links this library for the
+ * MSM entry points below instead of libblst's.  Each declaration cites the
+ * reference interface it replaces.
+ *
+ * Threading: entry points are thread-safe per call (each call uses its own
+ * device buffers; engine contexts are not shared across threads unless the
+ * caller serialises).  Errors: the blst-named functions keep blst's void
+ * signatures; on a HIP failure they print the error and abort (a silent wrong
+ * answer is never returned).  The msm_* extension API returns MSM_OK or a
+ * negative MSM_E* code and msm_last_error() describes it.
+ */
+#ifndef MSM_MI355X_H
+#define MSM_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- types: layout-identical to /root/reference/bindings/blst.h ---- */
+typedef uint8_t byte;                                      /* blst.h:53 */
+typedef uint64_t limb_t;                                   /* blst.h:54 */
+typedef struct { byte b[256 / 8]; } blst_scalar;           /* blst.h:56 */
+typedef struct { limb_t l[384 / 8 / sizeof(limb_t)]; } blst_fp;  /* blst.h:58 */
+typedef struct { blst_fp fp[2]; } blst_fp2;                /* blst.h:60 */
+typedef struct { blst_fp x, y, z; } blst_p1;               /* blst.h:164 */
+typedef struct { blst_fp x, y; } blst_p1_affine;           /* blst.h:165 */
+typedef struct { blst_fp2 x, y, z; } blst_p2;              /* blst.h:191 */
+typedef struct { blst_fp2 x, y; } blst_p2_affine;          /* blst.h:192 */
+typedef struct { blst_fp x, y, zzz, zz; } blst_p1xyzz;     /* blst.h:251 */
+typedef struct { blst_fp2 x, y, zzz, zz; } blst_p2xyzz;    /* blst.h:252 */
+typedef struct { int m; int b; int alpha; } digit_decomposition; /* blst.h:253 */
+
+/* ---- plain Pippenger (replaces src/multi_scalar.c:581-607, blst.h:238-246, :377-384) ----
+ * Same semantics as blst: points[] / scalars[] are arrays of pointers; when
+ * points[1] (resp. scalars[1]) is NULL the data is one flat array, scalars
+ * packed with stride (nbits+7)/8 (multi_scalar.c:393-416).  The low nbits bits
+ * of each scalar are used (scalars are not reduced mod r).  The all-zero
+ * affine point is infinity and contributes nothing.  ret is a Jacobian point
+ * in Montgomery form; any representative (callers normalise with to_affine).
+ * scratch is accepted for ABI compatibility and not used (device buffers are
+ * the engine's own).  Unlike blst (defect at n=1), any n >= 0 is exact. */
+size_t blst_p1s_mult_pippenger_scratch_sizeof(size_t npoints);
+void blst_p1s_mult_pippenger(blst_p1 *ret, const blst_p1_affine *const points[], size_t npoints,
+                             const byte *const scalars[], size_t nbits, limb_t *scratch);
+void blst_p1s_tile_pippenger(blst_p1 *ret, const blst_p1_affine *const points[], size_t npoints,
+                             const byte *const scalars[], size_t nbits, limb_t *scratch, size_t bit0,
+                             size_t window);
+size_t blst_p2s_mult_pippenger_scratch_sizeof(size_t npoints);
+void blst_p2s_mult_pippenger(blst_p2 *ret, const blst_p2_affine *const points[], size_t npoints,
+                             const byte *const scalars[], size_t nbits, limb_t *scratch);
+void blst_p2s_tile_pippenger(blst_p2 *ret, const blst_p2_affine *const points[], size_t npoints,
+                             const byte *const scalars[], size_t nbits, limb_t *scratch, size_t bit0,
+                             size_t window);
+
+/* ---- extension API: device-resident contexts (points uploaded once) ---- */
+enum {
+  MSM_OK = 0,
+  MSM_E_ARG = -1,      /* bad argument */
+  MSM_E_HIP = -2,      /* HIP runtime failure (message in msm_last_error) */
+  MSM_E_NODEV = -3,    /* no gfx950 device visible */
+  MSM_E_STATE = -4     /* context not ready (e.g. tables not built) */
+};
+typedef struct msm_ctx msm_ctx;
+const char *msm_last_error(void);
+int msm_device_count(void);
+/* group 1 (G1) or 2 (G2); points in blst affine layout, host or device memory */
+int msm_ctx_create(msm_ctx **ctx, int group, int device, int window_bits);
+int msm_ctx_set_points(msm_ctx *ctx, const void *points_affine, size_t npoints, int points_on_device,
+                       void *hip_stream);
+/* scalars: npoints byte strings with the given stride (32 for blst_scalar arrays),
+ * on host or device; ret: blst_p1 / blst_p2 Jacobian (host memory) */
+int msm_ctx_mult(msm_ctx *ctx, void *ret, const byte *scalars, size_t stride, size_t nbits, int scalars_on_device,
+                 void *hip_stream);
+int msm_ctx_set_profiling(msm_ctx *ctx, int on);
+/* per-phase device ms of the last msm_ctx_mult (profiling on):
+ * [digits, sort, accumulate, reduce, finalize, total] */
+int msm_ctx_phase_times(const msm_ctx *ctx, float out[6]);
+void msm_ctx_destroy(msm_ctx *ctx);
+
+/* ---- boundary helpers (host; no blst symbols are redefined) ---- */
+void msm_gen_scalars(byte *out32, size_t n, uint64_t seed);         /* BASELINE.md sec.3 SplitMix64 */
+void msm_p1_fixed_points(blst_p1_affine *out, size_t n);            /* P_i = 2^(i+1) G1 (main_p1.cpp:52-66) */
+void msm_p2_fixed_points(blst_p2_affine *out, size_t n);
+void msm_p1_to_affine(blst_p1_affine *out, const blst_p1 *in);      /* e1.c:80-92 */
+void msm_p2_to_affine(blst_p2_affine *out, const blst_p2 *in);
+void msm_p1_compress(byte out[48], const blst_p1 *in);              /* e1.c:225-234 */
+void msm_p2_compress(byte out[96], const blst_p2 *in);
+void msm_p1_add(blst_p1 *out, const blst_p1 *a, const blst_p1 *b);  /* Jacobian, doubling aware */
+void msm_p2_add(blst_p2 *out, const blst_p2 *a, const blst_p2 *b);
+
+/* ---- device self-test entry points (parity tests of the Fp/Fp2/xyzz layers) ----
+ * op: 0 mul, 1 add, 2 sub, 3 sqr; values in blst Montgomery layout */
+int msm_test_field(int group, int op, const limb_t *a, const limb_t *b, limb_t *out, size_t n);
+/* nseq sequences of len ops (point index | sign<<31, 0xffffffff = skip) -> per sequence
+ * two blst Jacobians: acc and acc+acc (via the xyzz+xyzz path) */
+int msm_test_xyzz(int group, const void *points_affine, size_t npoints, const uint32_t *ops, int len, size_t nseq,
+                  void *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

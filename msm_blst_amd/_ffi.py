@@ -1,0 +1,65 @@
+"""ctypes binding of libmsm_mi355x.so (include/msm_mi355x.h).
+
+The library is the product: loading fails loudly if it is missing or was
+built for another architecture -- there is no CPU fallback anywhere in
+msm_blst_amd.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmsm_mi355x.so")
+
+_lib = None
+
+
+class MsmError(RuntimeError):
+    pass
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MsmError(f"{LIB_PATH} not built: run `python -m msm_blst_amd.build` (hipcc, gfx950)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, sz, i32, u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64
+    for g in (1, 2):
+        f = getattr(L, f"blst_p{g}s_mult_pippenger")
+        f.argtypes = [vp, vp, sz, vp, sz, vp]
+        f.restype = None
+        f = getattr(L, f"blst_p{g}s_tile_pippenger")
+        f.argtypes = [vp, vp, sz, vp, sz, vp, sz, sz]
+        f.restype = None
+        f = getattr(L, f"blst_p{g}s_mult_pippenger_scratch_sizeof")
+        f.argtypes = [sz]
+        f.restype = sz
+        for name in (f"msm_p{g}_fixed_points",):
+            getattr(L, name).argtypes = [vp, sz]
+        for name in (f"msm_p{g}_to_affine", f"msm_p{g}_compress"):
+            getattr(L, name).argtypes = [vp, vp]
+        getattr(L, f"msm_p{g}_add").argtypes = [vp, vp, vp]
+    L.msm_last_error.restype = ctypes.c_char_p
+    L.msm_device_count.restype = i32
+    L.msm_ctx_create.argtypes = [ctypes.POINTER(vp), i32, i32, i32]
+    L.msm_ctx_set_points.argtypes = [vp, vp, sz, i32, vp]
+    L.msm_ctx_mult.argtypes = [vp, vp, vp, sz, sz, i32, vp]
+    L.msm_ctx_set_profiling.argtypes = [vp, i32]
+    L.msm_ctx_phase_times.argtypes = [vp, vp]
+    L.msm_ctx_destroy.argtypes = [vp]
+    L.msm_ctx_destroy.restype = None
+    L.msm_gen_scalars.argtypes = [vp, sz, u64]
+    L.msm_test_field.argtypes = [i32, i32, vp, vp, vp, sz]
+    L.msm_test_xyzz.argtypes = [i32, vp, sz, vp, i32, sz, vp]
+    for name in ("msm_ches_ctx_create",):
+        if hasattr(L, name):
+            pass
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != 0:
+        raise MsmError(f"msm_mi355x error {rc}: {lib().msm_last_error().decode(errors='replace')}")
+    return rc

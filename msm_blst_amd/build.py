@@ -1,0 +1,67 @@
+"""Build libmsm_mi355x.so (HIP, gfx950) in-tree.
+
+`python -m msm_blst_amd.build` or `msm_blst_amd.build.build()`.  Sources in
+msm_blst_amd/csrc are compiled with hipcc --offload-arch=gfx950 into objects
+under msm_blst_amd/_build/ and linked into msm_blst_amd/libmsm_mi355x.so.
+Rebuilds only what changed (mtime of sources and headers).
+"""
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+OBJ = os.path.join(HERE, "_build")
+LIB = os.path.join(HERE, "libmsm_mi355x.so")
+REPO = os.path.dirname(HERE)
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("MSM_OFFLOAD_ARCH", "gfx950")
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-value",
+         "-Wno-unused-function", f"-I{os.path.join(REPO, 'include')}"]
+SOURCES = ["engine.hip", "ches.hip", "abi.cpp"]
+
+
+def _deps():
+    return glob.glob(os.path.join(CSRC, "*.hpp")) + [os.path.join(REPO, "include", "msm_mi355x.h")]
+
+
+def _stale(target, inputs):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(i) > t for i in inputs if os.path.exists(i))
+
+
+def build(verbose=False, jobs=4):
+    os.makedirs(OBJ, exist_ok=True)
+    hdrs = _deps()
+    jobs_list = []
+    objs = []
+    for src in SOURCES:
+        sp = os.path.join(CSRC, src)
+        if not os.path.exists(sp):
+            continue
+        op = os.path.join(OBJ, os.path.splitext(src)[0] + ".o")
+        objs.append(op)
+        if _stale(op, [sp] + hdrs):
+            jobs_list.append([HIPCC] + FLAGS + ["-c", sp, "-o", op])
+
+    def run(cmd):
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        return r
+
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        list(ex.map(run, jobs_list))
+    if jobs_list or _stale(LIB, objs):
+        run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", LIB] + objs)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(verbose=True))

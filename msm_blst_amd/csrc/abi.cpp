@@ -1,0 +1,372 @@
+// abi.cpp -- extern "C" boundary of libmsm_mi355x.so (include/msm_mi355x.h).
+//
+// The blst-named entry points reproduce the reference's calling convention
+// (ref src/multi_scalar.c:581-607: arrays of pointers with the {ptr, NULL}
+// flat shortcut, scalars packed with stride (nbits+7)/8) and run the MSM on
+// the GPU; the msm_* functions expose device-resident contexts.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+
+#include "../../include/msm_mi355x.h"
+#include "engine.hpp"
+
+using namespace msm;
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+  g_err = msg;
+  return code;
+}
+
+int auto_window(size_t n) {
+  int lg = 0;
+  while (((size_t)1 << (lg + 1)) <= n) ++lg;
+  int c = lg - 4;
+  if (c < 8) c = 8;
+  if (c > 16) c = 16;
+  if (c == 9) c = 10;
+  if (c == 11) c = 12;
+  return c;
+}
+
+[[noreturn]] void die(const char *where, const std::exception &e) {
+  fprintf(stderr, "msm_mi355x: %s failed: %s\n", where, e.what());
+  fflush(stderr);
+  abort();
+}
+
+template <int G>
+Pippenger<G> &tls_engine(int window) {
+  thread_local std::map<std::pair<int, int>, std::unique_ptr<Pippenger<G>>> engines;
+  int dev = 0;
+  MSM_HIP_CHECK(hipGetDevice(&dev));
+  auto key = std::make_pair(dev, window);
+  auto it = engines.find(key);
+  if (it == engines.end()) it = engines.emplace(key, std::make_unique<Pippenger<G>>(dev, window)).first;
+  return *it->second;
+}
+
+// gather the {ptr,NULL}-or-pointer-array inputs into flat host arrays
+template <int G>
+void gather(std::vector<uint8_t> &pts, std::vector<uint8_t> &sc, const void *const *points, size_t n,
+            const byte *const *scalars, size_t nbits) {
+  const size_t psz = 96 * G, nb = (nbits + 7) / 8;
+  pts.resize(n * psz);
+  sc.resize(n * nb);
+  if (n == 0) return;
+  if (n == 1 || points[1] == nullptr) {
+    memcpy(pts.data(), points[0], n * psz);
+  } else {
+    for (size_t i = 0; i < n; ++i) memcpy(pts.data() + i * psz, points[i], psz);
+  }
+  if (n == 1 || scalars[1] == nullptr) {
+    memcpy(sc.data(), scalars[0], n * nb);
+  } else {
+    for (size_t i = 0; i < n; ++i) memcpy(sc.data() + i * nb, scalars[i], nb);
+  }
+}
+
+template <int G>
+void mult_pippenger(void *ret, const void *const *points, size_t n, const byte *const *scalars, size_t nbits) {
+  typedef typename HostField<G>::F HF;
+  hfp::Jac<HF> out;
+  if (n == 0) {
+    memset(&out, 0, sizeof out);
+    memcpy(ret, &out, sizeof out);
+    return;
+  }
+  std::vector<uint8_t> pts, sc;
+  gather<G>(pts, sc, points, n, scalars, nbits);
+  Pippenger<G> &eng = tls_engine<G>(auto_window(n));
+  hipStream_t s = 0;
+  eng.set_points(pts.data(), n, false, s);
+  DevBuf dsc;
+  dsc.ensure(sc.size() + 16);
+  MSM_HIP_CHECK(hipMemcpyAsync(dsc.p, sc.data(), sc.size(), hipMemcpyHostToDevice, s));
+  eng.run(s, dsc.as<uint8_t>(), (nbits + 7) / 8, (int)nbits, &out);
+  memcpy(ret, &out, sizeof out);
+}
+
+// one blst window tile (ref multi_scalar.c:383-419, 587-600): sum_i d_i P_i with
+// d_i the Booth digit of scalar i at [bit0, bit0+wbits) (lookback bit bit0-1).
+template <int G>
+void tile_pippenger(void *ret, const void *const *points, size_t n, const byte *const *scalars, size_t nbits,
+                    size_t bit0, size_t window) {
+  typedef typename HostField<G>::F HF;
+  size_t wbits, cbits;
+  if (bit0 + window > nbits) {
+    wbits = nbits - bit0;
+    cbits = wbits + 1;
+  } else {
+    wbits = cbits = window;
+  }
+  std::vector<uint8_t> pts, sc;
+  gather<G>(pts, sc, points, n, scalars, nbits);
+  const size_t nb = (nbits + 7) / 8, psz = 96 * G;
+  std::vector<uint8_t> small(n * 4, 0);
+  for (size_t i = 0; i < n; ++i) {
+    const uint8_t *s = sc.data() + i * nb;
+    uint32_t v = 0;
+    for (size_t k = 0; k <= wbits; ++k) {  // bits [bit0-1, bit0+wbits)
+      long b = (long)bit0 - 1 + (long)k;
+      if (b < 0 || (size_t)b >= nbits) continue;
+      v |= (uint32_t)((s[b / 8] >> (b % 8)) & 1) << k;
+    }
+    uint32_t sign = (v >> cbits) & 1;
+    int d = (int)((v + 1) >> 1);
+    if (sign) d -= 1 << cbits;
+    if (d < 0) {  // negate the point: y -> p - y
+      d = -d;
+      HF *y = reinterpret_cast<HF *>(pts.data() + i * psz + psz / 2);
+      *y = hfp::neg(*y);
+    }
+    memcpy(small.data() + i * 4, &d, 4);
+  }
+  Pippenger<G> &eng = tls_engine<G>(8);
+  hipStream_t st = 0;
+  eng.set_points(pts.data(), n, false, st);
+  DevBuf dsc;
+  dsc.ensure(small.size() + 16);
+  MSM_HIP_CHECK(hipMemcpyAsync(dsc.p, small.data(), small.size(), hipMemcpyHostToDevice, st));
+  hfp::Jac<HF> out;
+  eng.run(st, dsc.as<uint8_t>(), 4, (int)cbits + 1, &out);
+  memcpy(ret, &out, sizeof out);
+}
+
+size_t blst_window(size_t n) {  // ref multi_scalar.c:268-275
+  size_t w = 0;
+  while (n >>= 1) ++w;
+  return w > 12 ? w - 3 : (w > 4 ? w - 2 : (w ? 2 : 1));
+}
+}  // namespace
+
+template <class F>
+void fixed_points(hfp::Aff<F> *out, size_t n, hfp::Jac<F> g) {
+  std::vector<hfp::Jac<F>> j(n);
+  for (size_t i = 0; i < n; ++i) {
+    g = hfp::dbl(g);
+    j[i] = g;
+  }
+  hfp::to_affine_batch(out, j.data(), n);
+}
+
+struct msm_ctx {
+  int group = 1;
+  int device = 0;
+  std::unique_ptr<Pippenger<1>> g1;
+  std::unique_ptr<Pippenger<2>> g2;
+  DevBuf scalars;
+};
+
+extern "C" {
+
+size_t blst_p1s_mult_pippenger_scratch_sizeof(size_t npoints) { return sizeof(blst_p1xyzz) << (blst_window(npoints) - 1); }
+size_t blst_p2s_mult_pippenger_scratch_sizeof(size_t npoints) { return sizeof(blst_p2xyzz) << (blst_window(npoints) - 1); }
+
+void blst_p1s_mult_pippenger(blst_p1 *ret, const blst_p1_affine *const points[], size_t npoints,
+                             const byte *const scalars[], size_t nbits, limb_t *scratch) {
+  (void)scratch;
+  try {
+    mult_pippenger<1>(ret, (const void *const *)points, npoints, scalars, nbits);
+  } catch (const std::exception &e) {
+    die("blst_p1s_mult_pippenger", e);
+  }
+}
+void blst_p2s_mult_pippenger(blst_p2 *ret, const blst_p2_affine *const points[], size_t npoints,
+                             const byte *const scalars[], size_t nbits, limb_t *scratch) {
+  (void)scratch;
+  try {
+    mult_pippenger<2>(ret, (const void *const *)points, npoints, scalars, nbits);
+  } catch (const std::exception &e) {
+    die("blst_p2s_mult_pippenger", e);
+  }
+}
+void blst_p1s_tile_pippenger(blst_p1 *ret, const blst_p1_affine *const points[], size_t npoints,
+                             const byte *const scalars[], size_t nbits, limb_t *scratch, size_t bit0, size_t window) {
+  (void)scratch;
+  try {
+    tile_pippenger<1>(ret, (const void *const *)points, npoints, scalars, nbits, bit0, window);
+  } catch (const std::exception &e) {
+    die("blst_p1s_tile_pippenger", e);
+  }
+}
+void blst_p2s_tile_pippenger(blst_p2 *ret, const blst_p2_affine *const points[], size_t npoints,
+                             const byte *const scalars[], size_t nbits, limb_t *scratch, size_t bit0, size_t window) {
+  (void)scratch;
+  try {
+    tile_pippenger<2>(ret, (const void *const *)points, npoints, scalars, nbits, bit0, window);
+  } catch (const std::exception &e) {
+    die("blst_p2s_tile_pippenger", e);
+  }
+}
+
+const char *msm_last_error(void) { return g_err.c_str(); }
+
+int msm_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int msm_ctx_create(msm_ctx **ctx, int group, int device, int window_bits) {
+  if (!ctx || (group != 1 && group != 2)) return fail(MSM_E_ARG, "bad ctx/group");
+  if (msm_device_count() <= device || device < 0) return fail(MSM_E_NODEV, "no such HIP device");
+  try {
+    auto c = std::make_unique<msm_ctx>();
+    c->group = group;
+    c->device = device;
+    int wb = window_bits > 0 ? window_bits : 16;
+    if (group == 1) c->g1 = std::make_unique<Pippenger<1>>(device, wb);
+    else c->g2 = std::make_unique<Pippenger<2>>(device, wb);
+    *ctx = c.release();
+    return MSM_OK;
+  } catch (const std::exception &e) {
+    return fail(MSM_E_HIP, e.what());
+  }
+}
+
+int msm_ctx_set_points(msm_ctx *ctx, const void *points, size_t n, int on_device, void *stream) {
+  if (!ctx || (!points && n)) return fail(MSM_E_ARG, "bad args");
+  try {
+    if (ctx->group == 1) ctx->g1->set_points(points, n, on_device != 0, (hipStream_t)stream);
+    else ctx->g2->set_points(points, n, on_device != 0, (hipStream_t)stream);
+    return MSM_OK;
+  } catch (const std::exception &e) {
+    return fail(MSM_E_HIP, e.what());
+  }
+}
+
+int msm_ctx_mult(msm_ctx *ctx, void *ret, const byte *scalars, size_t stride, size_t nbits, int on_device,
+                 void *stream) {
+  if (!ctx || !ret || nbits == 0 || nbits > 256 || stride < (nbits + 7) / 8) return fail(MSM_E_ARG, "bad args");
+  try {
+    DeviceGuard g(ctx->device);
+    hipStream_t s = (hipStream_t)stream;
+    size_t n = ctx->group == 1 ? ctx->g1->npoints() : ctx->g2->npoints();
+    const uint8_t *d = scalars;
+    if (!on_device && n) {
+      ctx->scalars.ensure(n * stride + 16);
+      MSM_HIP_CHECK(hipMemcpyAsync(ctx->scalars.p, scalars, n * stride, hipMemcpyHostToDevice, s));
+      d = ctx->scalars.as<uint8_t>();
+    }
+    if (ctx->group == 1) {
+      hfp::Jac<hfp::Fp> out;
+      ctx->g1->run(s, d, stride, (int)nbits, &out);
+      memcpy(ret, &out, sizeof out);
+    } else {
+      hfp::Jac<hfp::Fp2> out;
+      ctx->g2->run(s, d, stride, (int)nbits, &out);
+      memcpy(ret, &out, sizeof out);
+    }
+    return MSM_OK;
+  } catch (const std::exception &e) {
+    return fail(MSM_E_HIP, e.what());
+  }
+}
+
+int msm_ctx_set_profiling(msm_ctx *ctx, int on) {
+  if (!ctx) return fail(MSM_E_ARG, "null ctx");
+  if (ctx->group == 1) ctx->g1->set_profiling(on != 0);
+  else ctx->g2->set_profiling(on != 0);
+  return MSM_OK;
+}
+
+int msm_ctx_phase_times(const msm_ctx *ctx, float out[6]) {
+  if (!ctx || !out) return fail(MSM_E_ARG, "null");
+  const PhaseTimes &t = ctx->group == 1 ? ctx->g1->times() : ctx->g2->times();
+  out[0] = t.digits;
+  out[1] = t.sort;
+  out[2] = t.accumulate;
+  out[3] = t.reduce;
+  out[4] = t.finalize;
+  out[5] = t.total;
+  return MSM_OK;
+}
+
+void msm_ctx_destroy(msm_ctx *ctx) { delete ctx; }
+
+// ---------------- boundary helpers ----------------
+static uint64_t splitmix64(uint64_t *s) {
+  uint64_t z = (*s += 0x9e3779b97f4a7c15ULL);
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+void msm_gen_scalars(byte *out, size_t n, uint64_t seed) {
+  static const uint64_t R[4] = {0xffffffff00000001ULL, 0x53bda402fffe5bfeULL, 0x3339d80809a1d805ULL,
+                                0x73eda753299d7d48ULL};
+  uint64_t st = seed;
+  for (size_t i = 0; i < n; ++i) {
+    uint64_t a[4];
+    for (;;) {
+      for (int k = 0; k < 4; ++k) a[k] = splitmix64(&st);
+      a[3] >>= 1;
+      bool lt = false;
+      for (int k = 3; k >= 0; --k) {
+        if (a[k] != R[k]) {
+          lt = a[k] < R[k];
+          break;
+        }
+      }
+      if (lt) break;
+    }
+    for (int k = 0; k < 32; ++k) out[32 * i + k] = (uint8_t)(a[k / 8] >> (8 * (k % 8)));
+  }
+}
+
+void msm_p1_fixed_points(blst_p1_affine *out, size_t n) {
+  fixed_points<hfp::Fp>(reinterpret_cast<hfp::Aff<hfp::Fp> *>(out), n, hfp::g1_generator());
+}
+void msm_p2_fixed_points(blst_p2_affine *out, size_t n) {
+  fixed_points<hfp::Fp2>(reinterpret_cast<hfp::Aff<hfp::Fp2> *>(out), n, hfp::g2_generator());
+}
+void msm_p1_to_affine(blst_p1_affine *out, const blst_p1 *in) {
+  *reinterpret_cast<hfp::Aff<hfp::Fp> *>(out) = hfp::to_affine(*reinterpret_cast<const hfp::Jac<hfp::Fp> *>(in));
+}
+void msm_p2_to_affine(blst_p2_affine *out, const blst_p2 *in) {
+  *reinterpret_cast<hfp::Aff<hfp::Fp2> *>(out) = hfp::to_affine(*reinterpret_cast<const hfp::Jac<hfp::Fp2> *>(in));
+}
+void msm_p1_compress(byte out[48], const blst_p1 *in) {
+  hfp::compress(out, hfp::to_affine(*reinterpret_cast<const hfp::Jac<hfp::Fp> *>(in)));
+}
+void msm_p2_compress(byte out[96], const blst_p2 *in) {
+  hfp::compress(out, hfp::to_affine(*reinterpret_cast<const hfp::Jac<hfp::Fp2> *>(in)));
+}
+void msm_p1_add(blst_p1 *out, const blst_p1 *a, const blst_p1 *b) {
+  *reinterpret_cast<hfp::Jac<hfp::Fp> *>(out) = hfp::addj(*reinterpret_cast<const hfp::Jac<hfp::Fp> *>(a),
+                                                          *reinterpret_cast<const hfp::Jac<hfp::Fp> *>(b));
+}
+void msm_p2_add(blst_p2 *out, const blst_p2 *a, const blst_p2 *b) {
+  *reinterpret_cast<hfp::Jac<hfp::Fp2> *>(out) = hfp::addj(*reinterpret_cast<const hfp::Jac<hfp::Fp2> *>(a),
+                                                           *reinterpret_cast<const hfp::Jac<hfp::Fp2> *>(b));
+}
+
+int msm_test_field(int group, int op, const limb_t *a, const limb_t *b, limb_t *out, size_t n) {
+  try {
+    if (group == 1) test_field<1>(op, a, b, out, n);
+    else test_field<2>(op, a, b, out, n);
+    return MSM_OK;
+  } catch (const std::exception &e) {
+    return fail(MSM_E_HIP, e.what());
+  }
+}
+int msm_test_xyzz(int group, const void *pts, size_t npts, const uint32_t *ops, int len, size_t nseq, void *out) {
+  try {
+    if (group == 1) test_xyzz<1>((const uint64_t *)pts, npts, ops, len, nseq, (uint64_t *)out);
+    else test_xyzz<2>((const uint64_t *)pts, npts, ops, len, nseq, (uint64_t *)out);
+    return MSM_OK;
+  } catch (const std::exception &e) {
+    return fail(MSM_E_HIP, e.what());
+  }
+}
+
+}  // extern "C"

@@ -1,0 +1,190 @@
+// ec.hpp -- BLS12-381 point arithmetic in xyzz coordinates for gfx950,
+// generic over the base field (G1: Fp, G2: Fp2).
+//
+// Replaces the reference's bucket formulas (src/ec_ops.h:642-785):
+//   xyzz_madd  <- POINTonE1xyzz_dadd_affine (ec_ops.h:710-769), madd-2008-s
+//                 with the sign twist and the mdbl-2008-s-1 doubling branch
+//   xyzz_add   <- POINTonE1xyzz_dadd (ec_ops.h:642-702), add-2008-s /
+//                 dbl-2008-s-1
+//   xyzz_dbl   <- the doubling branch of the above, used by the reductions
+// An xyzz point (X, Y, ZZZ, ZZ) stands for (X/ZZ, Y/ZZZ); infinity is ZZ == 0
+// (set exactly, never produced by a product).  Every coordinate leaving these
+// functions is in range class S (normalized, < 2p per component; fp.hpp).
+// Branches for the rare cases (P == +-bucket, infinity) are data-dependent
+// and divergent; random inputs never take them, the parity tests force them.
+#pragma once
+#include "fp.hpp"
+
+namespace msm {
+
+template <class F>
+struct Aff {
+  F x, y;
+};
+template <class F>
+struct Xyzz {
+  F x, y, zzz, zz;
+};
+
+template <class F>
+__device__ __forceinline__ bool xyzz_is_inf(const Xyzz<F> &a) {
+  return f_is_zero_exact(a.zz);
+}
+template <class F>
+__device__ __forceinline__ void xyzz_set_inf(Xyzz<F> &a) {
+  f_zero(a.x);
+  f_zero(a.y);
+  f_zero(a.zzz);
+  f_zero(a.zz);
+}
+// bucket := +-P   (ZZ = ZZZ = 1, Y negated instead of ZZZ; same point as the
+// reference's (X, Y, -1, 1) representative of ec_ops.h:720-724)
+template <class F>
+__device__ __forceinline__ void xyzz_from_aff(Xyzz<F> &r, const Aff<F> &p, bool neg) {
+  r.x = p.x;
+  if (neg) {
+    f_neg4(r.y, p.y);
+    f_nred(r.y);
+  } else {
+    r.y = p.y;
+  }
+  f_one(r.zzz);
+  f_one(r.zz);
+}
+
+// doubling of an xyzz point given in S (dbl-2008-s-1):
+//   U = 2Y, V = U^2, W = U V, S = X V, M = 3 X^2 (+ a ZZ^2, a = 0)
+//   X3 = M^2 - 2S, Y3 = M (S - X3) - W Y, ZZ3 = V ZZ, ZZZ3 = W ZZZ
+template <class F>
+__device__ __forceinline__ void xyzz_dbl(Xyzz<F> &r, const Xyzz<F> &a) {
+  if (xyzz_is_inf(a)) {
+    r = a;
+    return;
+  }
+  F U, V, W, S, M, t, X3, Y3;
+  f_add(U, a.y, a.y);      // < 4p lazy
+  f_sqr(V, U);             // S
+  f_mul(W, V, U);          // S
+  f_mul(S, a.x, V);        // S
+  f_sqr(M, a.x);           // S
+  f_mul3(M, M);            // < 6p lazy
+  f_sqr(X3, M);            // S
+  f_sub4(X3, X3, S);       // < 6p
+  f_norm(X3);
+  f_sub4(X3, X3, S);       // < 10p
+  f_nred(X3);              // S
+  f_sub4(t, S, X3);        // < 6p
+  f_mul(t, t, M);          // S
+  f_mul(Y3, W, a.y);       // S
+  f_sub4(Y3, t, Y3);       // < 6p
+  f_nred(Y3);              // S
+  f_mul(r.zz, V, a.zz);
+  f_mul(r.zzz, W, a.zzz);
+  r.x = X3;
+  r.y = Y3;
+}
+
+// acc += (neg ? -P : P); P affine, canonical, not infinity (callers skip the
+// all-zero affine point, as ec_ops.h:717 does).
+template <class F>
+__device__ __forceinline__ void xyzz_madd(Xyzz<F> &acc, const Aff<F> &p, bool neg) {
+  if (xyzz_is_inf(acc)) {
+    xyzz_from_aff(acc, p, neg);
+    return;
+  }
+  F y2, P, R, PP, PPP, Q, t;
+  if (neg) {
+    f_neg4(y2, p.y);       // < 4p, limbs < 2^29
+  } else {
+    y2 = p.y;
+  }
+  f_mul(P, p.x, acc.zz);   // U2 = X2 ZZ1          S
+  f_mul(R, y2, acc.zzz);   // S2 = Y2 ZZZ1         S
+  f_sub4(P, P, acc.x);     // P = U2 - X1          < 6p lazy
+  f_sub4(R, R, acc.y);     // R = S2 - Y1          < 6p lazy
+  f_sqr(PP, P);            // PP                   S
+  if (__builtin_expect(f_is_zero_S(PP), 0)) {
+    // X1 == X2: either P == bucket (double P) or P == -bucket (infinity)
+    F RR;
+    f_sqr(RR, R);
+    if (f_is_zero_S(RR)) {
+      Xyzz<F> b;
+      xyzz_from_aff(b, p, neg);
+      xyzz_dbl(acc, b);
+    } else {
+      xyzz_set_inf(acc);
+    }
+    return;
+  }
+  f_mul(PPP, PP, P);       // S
+  f_mul(Q, acc.x, PP);     // Q = X1 PP            S
+  F X3, Y3;
+  f_sqr(X3, R);            // R^2                  S
+  f_sub4(X3, X3, PPP);     // < 6p
+  f_norm(X3);
+  f_sub4(X3, X3, Q);       // < 10p
+  f_norm(X3);
+  f_sub4(X3, X3, Q);       // < 14p
+  f_nred(X3);              // X3 = R^2 - PPP - 2Q  S
+  f_sub4(t, Q, X3);        // < 6p
+  f_mul(t, t, R);          // R (Q - X3)           S
+  f_mul(Y3, acc.y, PPP);   // Y1 PPP               S
+  f_sub4(Y3, t, Y3);       // < 6p
+  f_nred(Y3);              // S
+  f_mul(acc.zz, acc.zz, PP);
+  f_mul(acc.zzz, acc.zzz, PPP);
+  acc.x = X3;
+  acc.y = Y3;
+}
+
+// acc += b, both xyzz in S
+template <class F>
+__device__ __forceinline__ void xyzz_add(Xyzz<F> &acc, const Xyzz<F> &b) {
+  if (xyzz_is_inf(b)) return;
+  if (xyzz_is_inf(acc)) {
+    acc = b;
+    return;
+  }
+  F U1, S1, P, R, PP, PPP, Q, t;
+  f_mul(U1, acc.x, b.zz);    // S
+  f_mul(S1, acc.y, b.zzz);   // S
+  f_mul(P, b.x, acc.zz);     // U2 S
+  f_mul(R, b.y, acc.zzz);    // S2 S
+  f_sub4(P, P, U1);          // < 6p
+  f_sub4(R, R, S1);          // < 6p
+  f_sqr(PP, P);
+  if (__builtin_expect(f_is_zero_S(PP), 0)) {
+    F RR;
+    f_sqr(RR, R);
+    if (f_is_zero_S(RR)) {
+      Xyzz<F> a = acc;
+      xyzz_dbl(acc, a);
+    } else {
+      xyzz_set_inf(acc);
+    }
+    return;
+  }
+  f_mul(PPP, PP, P);
+  f_mul(Q, U1, PP);
+  F X3, Y3;
+  f_sqr(X3, R);
+  f_sub4(X3, X3, PPP);
+  f_norm(X3);
+  f_sub4(X3, X3, Q);
+  f_norm(X3);
+  f_sub4(X3, X3, Q);
+  f_nred(X3);
+  f_sub4(t, Q, X3);
+  f_mul(t, t, R);
+  f_mul(Y3, S1, PPP);
+  f_sub4(Y3, t, Y3);
+  f_nred(Y3);
+  f_mul(acc.zz, acc.zz, b.zz);
+  f_mul(acc.zz, acc.zz, PP);
+  f_mul(acc.zzz, acc.zzz, b.zzz);
+  f_mul(acc.zzz, acc.zzz, PPP);
+  acc.x = X3;
+  acc.y = Y3;
+}
+
+}  // namespace msm

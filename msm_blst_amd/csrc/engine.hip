@@ -1,0 +1,277 @@
+// engine.hip -- host orchestration of the plain Pippenger pipeline on one
+// MI355X (see kernels.hpp for the kernels).  All launches go to the caller's
+// stream; the only host synchronisation is the final 16-window read-back.
+#include <hipcub/hipcub.hpp>
+
+#include "engine.hpp"
+#include "kernels.hpp"
+
+namespace msm {
+
+static inline unsigned nblk(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
+
+template <int G>
+Pippenger<G>::Pippenger(int device, int window_bits) : dev_(device), c_(window_bits) {
+  if (c_ < 8 || c_ > 20) throw std::runtime_error("window_bits out of range [8,20]");
+  DeviceGuard g(dev_);
+  ev_.resize(8);
+  for (auto &e : ev_) MSM_HIP_CHECK(hipEventCreate(&e));
+}
+template <int G>
+Pippenger<G>::~Pippenger() {
+  for (auto &e : ev_) (void)hipEventDestroy(e);
+}
+
+template <int G>
+void Pippenger<G>::set_points(const void *pts, size_t n, bool on_device, hipStream_t s) {
+  typedef typename FieldOf<G>::F F;
+  DeviceGuard g(dev_);
+  if (n == 0) {
+    n_ = 0;
+    return;
+  }
+  if (n >= (1ull << 31)) throw std::runtime_error("too many points");
+  size_t raw = n * 96 * G;
+  const void *src = pts;
+  if (!on_device) {
+    tmp_.ensure(raw);
+    MSM_HIP_CHECK(hipMemcpyAsync(tmp_.p, pts, raw, hipMemcpyHostToDevice, s));
+    src = tmp_.p;
+  }
+  pts_.ensure(n * sizeof(Aff<F>));
+  hipLaunchKernelGGL(k_convert_points<G>, dim3(nblk(n, 256)), dim3(256), 0, s, (const uint64_t *)src, pts_.as<Aff<F>>(),
+                     n);
+  MSM_HIP_CHECK(hipGetLastError());
+  n_ = n;
+}
+
+template <int C>
+static void launch_digits(hipStream_t s, const uint8_t *sc, size_t stride, size_t n, int nbits, int W, uint32_t *keys,
+                          uint32_t *ranks, uint32_t *counts) {
+  hipLaunchKernelGGL(k_digits<C>, dim3(nblk(n, 256)), dim3(256), 0, s, sc, stride, n, nbits, W, keys, ranks, counts);
+}
+template <int C>
+static void launch_scatter(hipStream_t s, const uint32_t *keys, const uint32_t *ranks, const uint32_t *off,
+                           uint32_t *sorted, size_t n, int W) {
+  hipLaunchKernelGGL(k_scatter<C>, dim3(nblk((size_t)W * n, 256)), dim3(256), 0, s, keys, ranks, off, sorted, n, W);
+}
+
+#define MSM_C_DISPATCH(c, FN, ...)                          \
+  switch (c) {                                              \
+    case 8: FN<8>(__VA_ARGS__); break;                      \
+    case 10: FN<10>(__VA_ARGS__); break;                    \
+    case 12: FN<12>(__VA_ARGS__); break;                    \
+    case 13: FN<13>(__VA_ARGS__); break;                    \
+    case 14: FN<14>(__VA_ARGS__); break;                    \
+    case 15: FN<15>(__VA_ARGS__); break;                    \
+    case 16: FN<16>(__VA_ARGS__); break;                    \
+    case 17: FN<17>(__VA_ARGS__); break;                    \
+    case 18: FN<18>(__VA_ARGS__); break;                    \
+    default: throw std::runtime_error("unsupported window"); \
+  }
+
+template <int G>
+void Pippenger<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, int nbits, hfp::Jac<HF> *out) {
+  typedef typename FieldOf<G>::F F;
+  DeviceGuard g(dev_);
+  if (nbits < 1 || nbits > 256) throw std::runtime_error("nbits must be in [1,256]");
+  const int c = c_;
+  const int W = (nbits + 1 + c - 1) / c;
+  const size_t NB = (size_t)1 << (c - 1);
+  const size_t NT = (size_t)W * NB;
+  hfp::Jac<HF> ret;
+  ret.x = hfp::fzero(HF());
+  ret.y = hfp::fzero(HF());
+  ret.z = hfp::fzero(HF());
+  if (n_ == 0) {
+    *out = ret;
+    return;
+  }
+  const size_t n = n_;
+  keys_.ensure((size_t)W * n * 4);
+  ranks_.ensure((size_t)W * n * 4);
+  sorted_.ensure((size_t)W * n * 4);
+  counts_.ensure(NT * 4);
+  offsets_.ensure(NT * 4);
+  order_.ensure(NT * 4);
+  iota_.ensure(NT * 4);
+  sortkeys_.ensure(NT * 4);
+  buckets_.ensure(NT * sizeof(Xyzz<F>));
+  redA_[0].ensure(NT / 2 * sizeof(Xyzz<F>) + 64);
+  redA_[1].ensure(NT / 2 * sizeof(Xyzz<F>) + 64);
+  redY_[0].ensure(NT / 2 * sizeof(Xyzz<F>) + 64);
+  redY_[1].ensure(NT / 2 * sizeof(Xyzz<F>) + 64);
+  fin_.ensure((size_t)W * 144 * G);
+
+  size_t scan_tmp = 0, sort_tmp = 0;
+  hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, counts_.as<uint32_t>(), offsets_.as<uint32_t>(), (int)NT, s);
+  hipcub::DeviceRadixSort::SortPairsDescending(nullptr, sort_tmp, counts_.as<uint32_t>(), sortkeys_.as<uint32_t>(),
+                                               iota_.as<uint32_t>(), order_.as<uint32_t>(), (int)NT, 0, 32, s);
+  tmp_.ensure(scan_tmp > sort_tmp ? scan_tmp : sort_tmp);
+
+  if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[0], s));
+  MSM_HIP_CHECK(hipMemsetAsync(counts_.p, 0, NT * 4, s));
+  MSM_C_DISPATCH(c, launch_digits, s, d_scalars, stride, n, nbits, W, keys_.as<uint32_t>(), ranks_.as<uint32_t>(),
+                 counts_.as<uint32_t>());
+  MSM_HIP_CHECK(hipGetLastError());
+  if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[1], s));
+  size_t tb = tmp_.bytes;
+  MSM_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp_.p, tb, counts_.as<uint32_t>(), offsets_.as<uint32_t>(), (int)NT, s));
+  MSM_C_DISPATCH(c, launch_scatter, s, keys_.as<uint32_t>(), ranks_.as<uint32_t>(), offsets_.as<uint32_t>(),
+                 sorted_.as<uint32_t>(), n, W);
+  hipLaunchKernelGGL(k_iota, dim3(nblk(NT, 256)), dim3(256), 0, s, iota_.as<uint32_t>(), NT);
+  tb = tmp_.bytes;
+  MSM_HIP_CHECK(hipcub::DeviceRadixSort::SortPairsDescending(tmp_.p, tb, counts_.as<uint32_t>(), sortkeys_.as<uint32_t>(),
+                                                             iota_.as<uint32_t>(), order_.as<uint32_t>(), (int)NT, 0, 32,
+                                                             s));
+  if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[2], s));
+  hipLaunchKernelGGL(k_accumulate<G>, dim3(nblk(NT, 256)), dim3(256), 0, s, order_.as<uint32_t>(),
+                     counts_.as<uint32_t>(), offsets_.as<uint32_t>(), sorted_.as<uint32_t>(), pts_.as<Aff<F>>(),
+                     buckets_.as<Xyzz<F>>(), NT);
+  MSM_HIP_CHECK(hipGetLastError());
+  if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[3], s));
+  // bucket reduction levels
+  const Xyzz<F> *A = buckets_.as<Xyzz<F>>();
+  const Xyzz<F> *Y = nullptr;
+  int S = (int)NB, lvl = 0;
+  while (S > 1) {
+    int L = S >= 8 ? 8 : S;
+    int log2L = L == 8 ? 3 : (L == 4 ? 2 : 1);
+    Xyzz<F> *A2 = redA_[lvl & 1].as<Xyzz<F>>();
+    Xyzz<F> *Y2 = redY_[lvl & 1].as<Xyzz<F>>();
+    size_t threads = (size_t)W * (S / L);
+    hipLaunchKernelGGL(k_reduce<G>, dim3(nblk(threads, 64)), dim3(64), 0, s, A, Y, A2, Y2, S, L, log2L, W);
+    MSM_HIP_CHECK(hipGetLastError());
+    A = A2;
+    Y = Y2;
+    S /= L;
+    ++lvl;
+  }
+  if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[4], s));
+  hipLaunchKernelGGL(k_finalize<G>, dim3(1), dim3(64), 0, s, Y, fin_.as<uint64_t>(), W);
+  MSM_HIP_CHECK(hipGetLastError());
+  std::vector<hfp::Jac<HF>> T(W);
+  MSM_HIP_CHECK(hipMemcpyAsync(T.data(), fin_.p, (size_t)W * sizeof(hfp::Jac<HF>), hipMemcpyDeviceToHost, s));
+  if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[5], s));
+  MSM_HIP_CHECK(hipStreamSynchronize(s));
+  // Horner over windows: ret = sum_w 2^(c w) T_w (ref multi_scalar.c:565-575)
+  ret = T[W - 1];
+  for (int w = W - 2; w >= 0; --w) {
+    for (int k = 0; k < c; ++k) ret = hfp::dbl(ret);
+    ret = hfp::addj(ret, T[w]);
+  }
+  *out = ret;
+  if (profile_) {
+    float ms;
+    MSM_HIP_CHECK(hipEventElapsedTime(&ms, ev_[0], ev_[1]));
+    times_.digits = ms;
+    MSM_HIP_CHECK(hipEventElapsedTime(&ms, ev_[1], ev_[2]));
+    times_.sort = ms;
+    MSM_HIP_CHECK(hipEventElapsedTime(&ms, ev_[2], ev_[3]));
+    times_.accumulate = ms;
+    MSM_HIP_CHECK(hipEventElapsedTime(&ms, ev_[3], ev_[4]));
+    times_.reduce = ms;
+    MSM_HIP_CHECK(hipEventElapsedTime(&ms, ev_[4], ev_[5]));
+    times_.finalize = ms;
+    MSM_HIP_CHECK(hipEventElapsedTime(&ms, ev_[0], ev_[5]));
+    times_.total = ms;
+    times_.accumulate_launches = 1;
+  }
+}
+
+template class Pippenger<1>;
+template class Pippenger<2>;
+
+// ---------------------------------------------------------------------------
+// device unit-test entry points (parity tests of the field / curve layers)
+// ---------------------------------------------------------------------------
+template <int G>
+__global__ void k_test_field(int op, const uint64_t *a, const uint64_t *b, uint64_t *out, size_t n) {
+  typedef typename FieldOf<G>::F F;
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  F x, y, r;
+  f_from_blst(x, a + i * 6 * G);
+  f_from_blst(y, b + i * 6 * G);
+  if (op == 0) {
+    f_mul(r, x, y);
+  } else if (op == 1) {
+    f_add(r, x, y);
+  } else if (op == 2) {
+    f_sub4(r, x, y);
+  } else {
+    f_sqr(r, x);
+  }
+  f_to_blst(out + i * 6 * G, r);
+}
+
+// xyzz sequences: thread i applies ops[i*len .. ] = (point index | sign<<31), then 2*acc via xyzz_add
+template <int G>
+__global__ void k_test_xyzz(const uint64_t *pts_blst, const uint32_t *ops, int len, size_t nseq, uint64_t *out) {
+  typedef typename FieldOf<G>::F F;
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nseq) return;
+  Xyzz<F> acc;
+  xyzz_set_inf(acc);
+  for (int k = 0; k < len; ++k) {
+    uint32_t o = ops[i * len + k];
+    if (o == 0xffffffffu) continue;
+    Aff<F> p;
+    const uint64_t *src = pts_blst + (size_t)(o & 0x7fffffffu) * 12 * G;
+    f_from_blst(p.x, src);
+    f_from_blst(p.y, src + 6 * G);
+    if (f_is_zero_exact(p.x) && f_is_zero_exact(p.y)) continue;
+    xyzz_madd(acc, p, (o >> 31) != 0);
+  }
+  Xyzz<F> acc2 = acc;
+  Xyzz<F> a1 = acc;
+  xyzz_add(acc2, a1);
+  Xyzz<F> res[2] = {acc, acc2};
+  for (int k = 0; k < 2; ++k) {
+    uint64_t *o = out + (i * 2 + k) * 18 * G;
+    if (xyzz_is_inf(res[k])) {
+      for (int j = 0; j < 18 * G; ++j) o[j] = 0;
+      continue;
+    }
+    F X, Y;
+    f_mul(X, res[k].x, res[k].zz);
+    f_mul(Y, res[k].y, res[k].zzz);
+    f_to_blst(o, X);
+    f_to_blst(o + 6 * G, Y);
+    f_to_blst(o + 12 * G, res[k].zz);
+  }
+}
+
+template <int G>
+void test_field(int op, const uint64_t *a, const uint64_t *b, uint64_t *out, size_t n) {
+  DevBuf da, db, dout;
+  size_t bytes = n * 48 * G;
+  da.ensure(bytes);
+  db.ensure(bytes);
+  dout.ensure(bytes);
+  MSM_HIP_CHECK(hipMemcpy(da.p, a, bytes, hipMemcpyHostToDevice));
+  MSM_HIP_CHECK(hipMemcpy(db.p, b, bytes, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_test_field<G>, dim3(nblk(n, 64)), dim3(64), 0, 0, op, da.as<uint64_t>(), db.as<uint64_t>(),
+                     dout.as<uint64_t>(), n);
+  MSM_HIP_CHECK(hipGetLastError());
+  MSM_HIP_CHECK(hipMemcpy(out, dout.p, bytes, hipMemcpyDeviceToHost));
+}
+template <int G>
+void test_xyzz(const uint64_t *pts, size_t npts, const uint32_t *ops, int len, size_t nseq, uint64_t *out) {
+  DevBuf dp, dops, dout;
+  dp.ensure(npts * 96 * G);
+  dops.ensure(nseq * len * 4 + 4);
+  dout.ensure(nseq * 2 * 144 * G);
+  MSM_HIP_CHECK(hipMemcpy(dp.p, pts, npts * 96 * G, hipMemcpyHostToDevice));
+  MSM_HIP_CHECK(hipMemcpy(dops.p, ops, nseq * len * 4, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_test_xyzz<G>, dim3(nblk(nseq, 64)), dim3(64), 0, 0, dp.as<uint64_t>(), dops.as<uint32_t>(), len,
+                     nseq, dout.as<uint64_t>());
+  MSM_HIP_CHECK(hipGetLastError());
+  MSM_HIP_CHECK(hipMemcpy(out, dout.p, nseq * 2 * 144 * G, hipMemcpyDeviceToHost));
+}
+template void test_field<1>(int, const uint64_t *, const uint64_t *, uint64_t *, size_t);
+template void test_field<2>(int, const uint64_t *, const uint64_t *, uint64_t *, size_t);
+template void test_xyzz<1>(const uint64_t *, size_t, const uint32_t *, int, size_t, uint64_t *);
+template void test_xyzz<2>(const uint64_t *, size_t, const uint32_t *, int, size_t, uint64_t *);
+
+}  // namespace msm

@@ -1,0 +1,301 @@
+// fp.hpp -- BLS12-381 base-field arithmetic for gfx950, kept in registers.
+//
+// Replaces the reference's Fp384 Montgomery routines (src/asm/mulx_mont_384-
+// x86_64.pl:1613-1828, add_mod_384-x86_64.pl:32-1000; portable spec
+// src/no_asm.h:29-291) and the Fp2 tower ops (no_asm.h:566-688).
+//
+// Design (measured on MI355X, tools/microbench/instr_rate.hip): one
+// v_mad_u64_u32 (32x32+64 -> 64) issues at the same rate as one
+// v_add_co_u32, so the cost of a multi-precision product is set by how many
+// carry instructions surround each mad.  We therefore use 14 limbs of 28
+// bits (392 bits, radix 2^28, Montgomery R = 2^392) instead of the 6x64-bit
+// layout of blst: every 28x28 product is < 2^56 and a whole product-scanning
+// column (<= 28 terms, limbs < 2^30) fits in one 64-bit accumulator, so each
+// limb product is exactly ONE v_mad_u64_u32 with no carry handling (FIPS
+// Montgomery: 392 mads + ~4 ops per column).
+//
+// Values are kept lazily reduced: a Montgomery product of inputs < 2^386 is
+// < 2p, adds do no carry propagation (limbs < 2^30 stay legal mul inputs),
+// subtraction adds a limb-wise "borrow-adjusted" multiple of p (every limb
+// >= 2^28-1) so no limb goes negative.  Range invariants are documented at
+// each use in ec.hpp.  Canonical values (< p) are produced only at the
+// boundary (fp_canon).  The 6x64-bit blst layout is used in HBM at the C-ABI
+// boundary and converted once per point on upload.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace msm {
+
+constexpr int NL = 14;            // limbs
+constexpr uint32_t MASK = 0x0fffffffu;
+constexpr uint32_t N0P = 0x0ffcfffdu;  // -p^-1 mod 2^28
+
+// p in radix 2^28
+__device__ constexpr uint32_t P28[NL] = {0xfffaaab, 0xfefffff, 0x3ffffb9, 0xfffeb15, 0x6241eab, 0xa0f6b0f, 0xf6730d2,
+                                         0xf38512b, 0x4774b84, 0x4bacd76, 0xba7b643, 0xe69a4b1, 0x1ea397f, 0x001a011};
+// k*p with limbs borrow-adjusted so limbs 0..12 are >= 2^28-1 (subtrahend headroom)
+__device__ constexpr uint32_t SUB4P[NL] = {0x1ffeaaac, 0x1fbffffe, 0x1ffffee6, 0x1fffac53, 0x18907aae,
+                                           0x183dac3c, 0x1d9cc349, 0x1ce144ae, 0x11dd2e12, 0x12eb35d8,
+                                           0x1e9ed90c, 0x19a692c5, 0x17a8e5fe, 0x0068043};
+__device__ constexpr uint32_t SUB8P[NL] = {0x1ffd5558, 0x1f7ffffe, 0x1ffffdce, 0x1fff58a8, 0x1120f55e,
+                                           0x107b587a, 0x1b398694, 0x19c2895e, 0x13ba5c26, 0x15d66bb1,
+                                           0x1d3db219, 0x134d258c, 0x1f51cbfe, 0x00d0087};
+__device__ constexpr uint32_t SUB16P[NL] = {0x1ffaaab0, 0x1efffffe, 0x1ffffb9e, 0x1ffeb152, 0x1241eabe,
+                                            0x10f6b0f5, 0x16730d29, 0x138512be, 0x1774b84e, 0x1bacd763,
+                                            0x1a7b6433, 0x169a4b1a, 0x1ea397fd, 0x01a0110};
+__device__ constexpr uint32_t SUB32P[NL] = {0x1ff55560, 0x1dfffffe, 0x1ffff73e, 0x1ffd62a6, 0x1483d57e,
+                                            0x11ed61eb, 0x1ce61a53, 0x170a257d, 0x1ee9709d, 0x1759aec7,
+                                            0x14f6c868, 0x1d349636, 0x1d472ffb, 0x0340222};
+// 2^392 mod p (one), 2^400 mod p (blst -> internal), 2^384 mod p (internal -> blst)
+__device__ constexpr uint32_t ONE28[NL] = {0x347fcb8, 0xd800000, 0x002b119, 0x0cde6d2, 0xc7212e0, 0x83a2090, 0x037669f,
+                                           0xda0f73e, 0x9b09b42, 0x1297bb0, 0x515d98f, 0x012ca7c, 0x659fcfa, 0x000577a};
+__device__ constexpr uint32_t TOINT28[NL] = {0x80e6299, 0x3500034, 0xeb12856, 0xdeb2699, 0xc988670,
+                                             0x4ef6697, 0x70983e8, 0xa4e6fe9, 0x3e8a053, 0xecf271e,
+                                             0xc20d323, 0x6eb6385, 0x47f1286, 0x00156da};
+__device__ constexpr uint32_t FROMINT28[NL] = {0x002fffd, 0x0900000, 0xc000276, 0x000bc40, 0x8baebf4,
+                                               0x5753c75, 0x55f4898, 0x7052574, 0x7ce5853, 0x56ec6d7,
+                                               0x71a97a2, 0xe4935c0, 0xec3fa80, 0x0015f65};
+
+struct Fp {
+  uint32_t v[NL];
+};
+
+__device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
+  return (uint64_t)a * (uint64_t)b + c;  // -> v_mad_u64_u32
+}
+
+// Montgomery product, FIPS (finely integrated product scanning).
+// Inputs: limbs < 2^30, values with a*b < 2^392 * p (e.g. both < 2^386).
+// Output: normalized limbs (< 2^28), value < 2p.
+__device__ __forceinline__ void fp_mul(Fp &r, const Fp &a, const Fp &b) {
+  uint32_t m[NL];
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {
+#pragma unroll
+    for (int i = 0; i <= k; ++i) acc = mad64(a.v[i], b.v[k - i], acc);
+#pragma unroll
+    for (int i = 0; i < k; ++i) acc = mad64(m[i], P28[k - i], acc);
+    m[k] = ((uint32_t)acc * N0P) & MASK;
+    acc = mad64(m[k], P28[0], acc);
+    acc >>= 28;
+  }
+#pragma unroll
+  for (int k = NL; k < 2 * NL - 1; ++k) {
+#pragma unroll
+    for (int i = k - NL + 1; i < NL; ++i) acc = mad64(a.v[i], b.v[k - i], acc);
+#pragma unroll
+    for (int i = k - NL + 1; i < NL; ++i) acc = mad64(m[i], P28[k - i], acc);
+    r.v[k - NL] = (uint32_t)acc & MASK;
+    acc >>= 28;
+  }
+  r.v[NL - 1] = (uint32_t)acc;
+}
+
+// Montgomery square: cross products once, doubled (limbs < 2^29 so 2a_i < 2^30).
+__device__ __forceinline__ void fp_sqr(Fp &r, const Fp &a) {
+  uint32_t m[NL], a2[NL];
+#pragma unroll
+  for (int i = 0; i < NL; ++i) a2[i] = a.v[i] << 1;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {
+#pragma unroll
+    for (int i = 0; 2 * i < k; ++i) acc = mad64(a2[i], a.v[k - i], acc);
+    if ((k & 1) == 0) acc = mad64(a.v[k / 2], a.v[k / 2], acc);
+#pragma unroll
+    for (int i = 0; i < k; ++i) acc = mad64(m[i], P28[k - i], acc);
+    m[k] = ((uint32_t)acc * N0P) & MASK;
+    acc = mad64(m[k], P28[0], acc);
+    acc >>= 28;
+  }
+#pragma unroll
+  for (int k = NL; k < 2 * NL - 1; ++k) {
+#pragma unroll
+    for (int i = k - NL + 1; 2 * i < k; ++i) acc = mad64(a2[i], a.v[k - i], acc);
+    if ((k & 1) == 0) acc = mad64(a.v[k / 2], a.v[k / 2], acc);
+#pragma unroll
+    for (int i = k - NL + 1; i < NL; ++i) acc = mad64(m[i], P28[k - i], acc);
+    r.v[k - NL] = (uint32_t)acc & MASK;
+    acc >>= 28;
+  }
+  r.v[NL - 1] = (uint32_t)acc;
+}
+
+// lazy add: no carry propagation
+__device__ __forceinline__ void fp_add(Fp &r, const Fp &a, const Fp &b) {
+#pragma unroll
+  for (int i = 0; i < NL; ++i) r.v[i] = a.v[i] + b.v[i];
+}
+// carry propagation -> limbs < 2^28 (value unchanged, non-negative limbs assumed)
+__device__ __forceinline__ void fp_norm(Fp &a) {
+#pragma unroll
+  for (int i = 0; i < NL - 1; ++i) {
+    a.v[i + 1] += a.v[i] >> 28;
+    a.v[i] &= MASK;
+  }
+}
+// r = a + K*p - b, K in {4,8,16,32}; b must be normalized (limbs < 2^28) with b < K*p/2-ish
+// (precisely: b's top limb below the adjusted top limb of K*p).
+template <int K>
+__device__ __forceinline__ void fp_sub(Fp &r, const Fp &a, const Fp &b) {
+  const uint32_t *C = K == 4 ? SUB4P : K == 8 ? SUB8P : K == 16 ? SUB16P : SUB32P;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) r.v[i] = a.v[i] + C[i] - b.v[i];
+}
+// r = K*p - a (negation), a normalized
+template <int K>
+__device__ __forceinline__ void fp_neg(Fp &r, const Fp &a) {
+  const uint32_t *C = K == 4 ? SUB4P : K == 8 ? SUB8P : K == 16 ? SUB16P : SUB32P;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) r.v[i] = C[i] - a.v[i];
+}
+__device__ __forceinline__ void fp_cneg4(Fp &r, const Fp &a, bool neg) {
+#pragma unroll
+  for (int i = 0; i < NL; ++i) r.v[i] = neg ? SUB4P[i] - a.v[i] : a.v[i];
+}
+__device__ __forceinline__ void fp_set(Fp &r, const uint32_t *c) {
+#pragma unroll
+  for (int i = 0; i < NL; ++i) r.v[i] = c[i];
+}
+__device__ __forceinline__ void fp_zero(Fp &r) {
+#pragma unroll
+  for (int i = 0; i < NL; ++i) r.v[i] = 0;
+}
+__device__ __forceinline__ void fp_one(Fp &r) { fp_set(r, ONE28); }
+__device__ __forceinline__ bool fp_is_zero_exact(const Fp &a) {
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) o |= a.v[i];
+  return o == 0;
+}
+// a normalized with a < 2p: a == 0 mod p  <=>  a == 0 or a == p
+__device__ __forceinline__ bool fp_is_zero_lt2p(const Fp &a) {
+  uint32_t o = 0, x = 0;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    o |= a.v[i];
+    x |= a.v[i] ^ P28[i];
+  }
+  return o == 0 || x == 0;
+}
+// conditional subtract p for normalized a < 2p -> canonical [0,p)
+__device__ __forceinline__ void fp_csub_p(Fp &a) {
+  uint32_t t[NL];
+  int32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    int32_t d = (int32_t)a.v[i] - (int32_t)P28[i] + br;
+    br = d >> 28;          // arithmetic shift: 0 or -1
+    t[i] = (uint32_t)d & MASK;
+  }
+  bool ge = br == 0;       // no final borrow -> a >= p
+#pragma unroll
+  for (int i = 0; i < NL; ++i) a.v[i] = ge ? t[i] : a.v[i];
+}
+// canonical representative of any lazy value (< 2^386, limbs < 2^30):
+// multiply by one (=2^392 mod p, Montgomery one) keeps the value, result < 2p normalized.
+__device__ __forceinline__ void fp_canon(Fp &r, const Fp &a) {
+  Fp one;
+  fp_one(one);
+  fp_mul(r, a, one);
+  fp_csub_p(r);
+}
+
+// Reduce a normalized value v < 32p to [0, 2p) (class S): quotient estimate
+// from the top limb, q = floor(v13 * floor(2^32/(p13+1)) / 2^32) <= floor(v/p);
+// v - q*p < 1.0003p (verified exhaustively over the top limb in DESIGN.md).
+constexpr uint32_t RED_MAG = 0x9d83;  // floor(2^32 / (p13 + 1)), p13 = 0x1a011
+__device__ __forceinline__ void fp_red(Fp &a) {
+  uint32_t q = (uint32_t)(((uint64_t)a.v[NL - 1] * RED_MAG) >> 32);
+  int64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    int64_t t = (int64_t)a.v[i] - (int64_t)((uint64_t)q * P28[i]) + c;
+    a.v[i] = (uint32_t)t & MASK;
+    c = t >> 28;
+  }
+}
+// normalize then reduce: lazy value (< 32p, limbs < 2^31, non-negative) -> class S
+__device__ __forceinline__ void fp_nred(Fp &a) {
+  fp_norm(a);
+  fp_red(a);
+}
+
+// ------------------------------------------------------------ generic API ---
+// Range classes used by ec.hpp (all values non-negative):
+//   S : normalized limbs (< 2^28), value < 2p.  Every f_mul/f_sqr output, every
+//       f_nred output, every stored coordinate.
+//   lazy : limbs < 2^30, value < 40p.  Legal f_mul/f_sqr input.
+//   f_add(S,S) < 4p lazy; f_sub4(x,S) = x + 4p - S (x S -> < 6p lazy);
+//   f_sub subtrahend MUST be S.
+__device__ __forceinline__ void f_mul(Fp &r, const Fp &a, const Fp &b) { fp_mul(r, a, b); }
+__device__ __forceinline__ void f_sqr(Fp &r, const Fp &a) { fp_sqr(r, a); }
+__device__ __forceinline__ void f_add(Fp &r, const Fp &a, const Fp &b) { fp_add(r, a, b); }
+__device__ __forceinline__ void f_sub4(Fp &r, const Fp &a, const Fp &b) { fp_sub<4>(r, a, b); }
+__device__ __forceinline__ void f_nred(Fp &a) { fp_nred(a); }
+__device__ __forceinline__ void f_norm(Fp &a) { fp_norm(a); }
+__device__ __forceinline__ void f_neg4(Fp &r, const Fp &a) { fp_neg<4>(r, a); }
+__device__ __forceinline__ void f_one(Fp &r) { fp_one(r); }
+__device__ __forceinline__ void f_zero(Fp &r) { fp_zero(r); }
+__device__ __forceinline__ bool f_is_zero_exact(const Fp &a) { return fp_is_zero_exact(a); }
+__device__ __forceinline__ bool f_is_zero_S(const Fp &a) { return fp_is_zero_lt2p(a); }
+// 3a for a in S -> lazy (< 6p, limbs < 2^30)
+__device__ __forceinline__ void f_mul3(Fp &r, const Fp &a) {
+#pragma unroll
+  for (int i = 0; i < NL; ++i) r.v[i] = a.v[i] * 3u;
+}
+
+// ---------------------------------------------------------------- Fp2 ----
+struct Fp2 {
+  Fp c0, c1;
+};
+
+// Karatsuba (ref no_asm.h:566-579): 3 Montgomery products, outputs reduced to S.
+__device__ __forceinline__ void f_mul(Fp2 &r, const Fp2 &a, const Fp2 &b) {
+  Fp t0, t1, sa, sb, t2;
+  fp_mul(t0, a.c0, b.c0);
+  fp_mul(t1, a.c1, b.c1);
+  fp_add(sa, a.c0, a.c1);
+  fp_add(sb, b.c0, b.c1);
+  fp_norm(sa);                     // component limbs may be < 2^29.6 (sub4 outputs): keep
+  fp_norm(sb);                     // mul-input limbs < 2^30 (column bound, see fp_mul)
+  fp_mul(t2, sa, sb);
+  fp_sub<4>(r.c0, t0, t1);
+  fp_nred(r.c0);
+  fp_sub<4>(t2, t2, t0);
+  fp_norm(t2);
+  fp_sub<4>(r.c1, t2, t1);
+  fp_nred(r.c1);
+}
+// (a0 + a1 i)^2 = (a0+a1)(a0-a1) + 2 a0 a1 i   (ref no_asm.h:638-688)
+__device__ __forceinline__ void f_sqr(Fp2 &r, const Fp2 &a) {
+  Fp s, d, m, a1 = a.c1;
+  fp_norm(a1);
+  fp_add(s, a.c0, a.c1);
+  fp_sub<32>(d, a.c0, a1);
+  fp_mul(m, a.c0, a.c1);
+  fp_mul(r.c0, s, d);
+  fp_add(r.c1, m, m);
+  fp_red(r.c1);  // m + m < 4p with limbs < 2^29: red handles non-normalized limbs via signed carry
+  fp_norm(r.c1);
+}
+__device__ __forceinline__ void f_add(Fp2 &r, const Fp2 &a, const Fp2 &b) {
+  fp_add(r.c0, a.c0, b.c0);
+  fp_add(r.c1, a.c1, b.c1);
+}
+__device__ __forceinline__ void f_sub4(Fp2 &r, const Fp2 &a, const Fp2 &b) {
+  fp_sub<4>(r.c0, a.c0, b.c0);
+  fp_sub<4>(r.c1, a.c1, b.c1);
+}
+__device__ __forceinline__ void f_nred(Fp2 &a) { fp_nred(a.c0); fp_nred(a.c1); }
+__device__ __forceinline__ void f_norm(Fp2 &a) { fp_norm(a.c0); fp_norm(a.c1); }
+__device__ __forceinline__ void f_neg4(Fp2 &r, const Fp2 &a) { fp_neg<4>(r.c0, a.c0); fp_neg<4>(r.c1, a.c1); }
+__device__ __forceinline__ void f_one(Fp2 &r) { fp_one(r.c0); fp_zero(r.c1); }
+__device__ __forceinline__ void f_zero(Fp2 &r) { fp_zero(r.c0); fp_zero(r.c1); }
+__device__ __forceinline__ bool f_is_zero_exact(const Fp2 &a) { return fp_is_zero_exact(a.c0) && fp_is_zero_exact(a.c1); }
+__device__ __forceinline__ bool f_is_zero_S(const Fp2 &a) { return fp_is_zero_lt2p(a.c0) && fp_is_zero_lt2p(a.c1); }
+__device__ __forceinline__ void f_mul3(Fp2 &r, const Fp2 &a) { f_mul3(r.c0, a.c0); f_mul3(r.c1, a.c1); }
+
+}  // namespace msm

@@ -1,0 +1,303 @@
+// kernels.hpp -- HIP kernels of the MSM engine (gfx950).  Templated on the
+// group: G1 (F = Fp) and G2 (F = Fp2).
+//
+// Plain Pippenger pipeline (replaces ref src/multi_scalar.c:383-419 tile /
+// :281-297 integrate / :549-576 window loop):
+//   k_digits      signed c-bit window digits of every scalar, per-bucket
+//                 histogram (atomics) + each entry's rank within its bucket
+//   k_scatter     counting-sort placement: sorted[off[bucket] + rank] = point
+//   (hipcub)      exclusive scan of counts; bucket schedule = ids sorted by
+//                 count, descending, so a wavefront's 64 buckets are equally long
+//   k_accumulate  one lane per bucket: xyzz += +-P over its sorted points
+//   k_reduce      segmented running sums, log_L(NB) levels (sum_b b*B_b)
+//   k_finalize    window totals -> blst Jacobian (R=2^384 Montgomery)
+// CHES pipeline: see ches.hpp.
+#pragma once
+#include "ec.hpp"
+
+namespace msm {
+
+template <int G>
+struct FieldOf;
+template <>
+struct FieldOf<1> {
+  typedef Fp F;
+};
+template <>
+struct FieldOf<2> {
+  typedef Fp2 F;
+};
+
+// ---- wide (16 B) loads/stores of POD structs whose size is a multiple of 16 ----
+template <class T>
+__device__ __forceinline__ T ld16(const T *p) {
+  static_assert(sizeof(T) % 16 == 0, "16B multiple");
+  T r;
+  const uint4 *s = reinterpret_cast<const uint4 *>(p);
+  uint4 tmp[sizeof(T) / 16];
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 16); ++i) tmp[i] = s[i];
+  __builtin_memcpy(&r, tmp, sizeof(T));
+  return r;
+}
+template <class T>
+__device__ __forceinline__ void st16(T *p, const T &v) {
+  static_assert(sizeof(T) % 16 == 0, "16B multiple");
+  uint4 tmp[sizeof(T) / 16];
+  __builtin_memcpy(tmp, &v, sizeof(T));
+  uint4 *d = reinterpret_cast<uint4 *>(p);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 16); ++i) d[i] = tmp[i];
+}
+
+// ---- blst 6x64 LE  <->  14 x 28-bit limbs ----
+__device__ __forceinline__ void unpack384(Fp &r, const uint64_t *l) {
+  uint32_t w[12];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    w[2 * i] = (uint32_t)l[i];
+    w[2 * i + 1] = (uint32_t)(l[i] >> 32);
+  }
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {
+    const int bit = 28 * k, wi = bit / 32, sh = bit % 32;
+    uint32_t lo = wi < 12 ? w[wi] : 0u;
+    uint32_t hi = wi + 1 < 12 ? w[wi + 1] : 0u;
+    uint64_t v = ((uint64_t)hi << 32) | lo;
+    r.v[k] = (uint32_t)(v >> sh) & MASK;
+  }
+}
+__device__ __forceinline__ void pack384(uint64_t *l, const Fp &a) {  // a normalized, < 2^384
+  uint32_t w[12];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) w[i] = 0;
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {
+    const int bit = 28 * k, wi = bit / 32, sh = bit % 32;
+    uint64_t v = (uint64_t)a.v[k] << sh;
+    if (wi < 12) w[wi] |= (uint32_t)v;
+    if (wi + 1 < 12) w[wi + 1] |= (uint32_t)(v >> 32);
+  }
+#pragma unroll
+  for (int i = 0; i < 6; ++i) l[i] = (uint64_t)w[2 * i] | ((uint64_t)w[2 * i + 1] << 32);
+}
+// blst Montgomery (R=2^384, canonical) -> internal (R=2^392, canonical)
+__device__ __forceinline__ void fp_from_blst(Fp &r, const uint64_t *l) {
+  Fp a, k;
+  unpack384(a, l);
+  fp_set(k, TOINT28);
+  fp_mul(r, a, k);
+  fp_csub_p(r);
+}
+// internal (any class-S / lazy value) -> blst Montgomery canonical
+__device__ __forceinline__ void fp_to_blst(uint64_t *l, const Fp &a) {
+  Fp k, r;
+  fp_set(k, FROMINT28);
+  fp_mul(r, a, k);
+  fp_csub_p(r);
+  pack384(l, r);
+}
+__device__ __forceinline__ void f_from_blst(Fp &r, const uint64_t *l) { fp_from_blst(r, l); }
+__device__ __forceinline__ void f_from_blst(Fp2 &r, const uint64_t *l) {
+  fp_from_blst(r.c0, l);
+  fp_from_blst(r.c1, l + 6);
+}
+__device__ __forceinline__ void f_to_blst(uint64_t *l, const Fp &a) { fp_to_blst(l, a); }
+__device__ __forceinline__ void f_to_blst(uint64_t *l, const Fp2 &a) {
+  fp_to_blst(l, a.c0);
+  fp_to_blst(l + 6, a.c1);
+}
+
+// ---------------------------------------------------------------------------
+// point conversion: blst affine (Montgomery R=2^384) -> internal affine limbs
+// ---------------------------------------------------------------------------
+template <int G>
+__global__ void k_convert_points(const uint64_t *__restrict__ in, Aff<typename FieldOf<G>::F> *__restrict__ out,
+                                 size_t n) {
+  typedef typename FieldOf<G>::F F;
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t *p = in + i * 12 * G;
+  Aff<F> a;
+  f_from_blst(a.x, p);
+  f_from_blst(a.y, p + 6 * G);
+  st16(&out[i], a);
+}
+
+// ---------------------------------------------------------------------------
+// signed window digits (ref ec_mult.h:23-55 booth encoding, generalised):
+// window w covers bits [w*c, w*c+c); raw = bits + carry; raw > 2^(c-1) ->
+// digit raw - 2^c with carry 1.  The top window never carries because
+// W*c >= nbits + 1.  Entry key = (bucket-1) | sign<<31, or ~0 for digit 0.
+// ---------------------------------------------------------------------------
+constexpr uint32_t KEY_NONE = 0xffffffffu;
+
+__device__ __forceinline__ uint32_t scalar_bits(const uint32_t s[10], int off, int c) {
+  int wi = off >> 5, sh = off & 31;
+  uint64_t v = (uint64_t)s[wi] | ((uint64_t)s[wi + 1] << 32);
+  return (uint32_t)(v >> sh) & ((1u << c) - 1u);
+}
+
+template <int C>
+__global__ void k_digits(const uint8_t *__restrict__ scalars, size_t stride, size_t n, int nbits, int W,
+                         uint32_t *__restrict__ keys, uint32_t *__restrict__ ranks, uint32_t *__restrict__ counts) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  constexpr uint32_t NB = 1u << (C - 1);
+  const uint8_t *sp = scalars + i * stride;
+  int nbytes = (nbits + 7) / 8;
+  uint32_t s[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) s[k] = 0;
+  if (stride % 4 == 0 && nbytes == 32) {
+    const uint32_t *s32 = reinterpret_cast<const uint32_t *>(sp);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s[k] = s32[k];
+  } else {
+    for (int b = 0; b < nbytes; ++b) s[b >> 2] |= (uint32_t)sp[b] << (8 * (b & 3));
+  }
+  // keep only the low nbits bits (ref multi_scalar.c:396 wmask semantics)
+  if (nbits < 256) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      int lo = 32 * k;
+      if (nbits <= lo) s[k] = 0;
+      else if (nbits < lo + 32) s[k] &= (1u << (nbits - lo)) - 1u;
+    }
+  }
+  uint32_t carry = 0;
+  constexpr int WMAX = (257 + C - 1) / C;
+#pragma unroll
+  for (int w = 0; w < WMAX; ++w) {
+    if (w < W) {
+      uint32_t raw = scalar_bits(s, w * C, C) + carry;
+      uint32_t b, sign;
+      if (w < W - 1 && raw > NB) {
+        b = (1u << C) - raw;
+        sign = 1;
+        carry = 1;
+      } else {
+        b = raw;
+        sign = 0;
+        carry = 0;
+      }
+      size_t e = (size_t)w * n + i;
+      if (b) {
+        uint32_t bi = b - 1;
+        ranks[e] = atomicAdd(&counts[(size_t)w * NB + bi], 1u);
+        keys[e] = bi | (sign << 31);
+      } else {
+        keys[e] = KEY_NONE;
+      }
+    }
+  }
+}
+
+template <int C>
+__global__ void k_scatter(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ ranks,
+                          const uint32_t *__restrict__ offsets, uint32_t *__restrict__ sorted, size_t n, int W) {
+  size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (size_t)W * n) return;
+  uint32_t k = keys[e];
+  if (k == KEY_NONE) return;
+  constexpr uint32_t NB = 1u << (C - 1);
+  size_t w = e / n, i = e - w * n;
+  uint32_t pos = offsets[w * NB + (k & 0x7fffffffu)] + ranks[e];
+  sorted[pos] = (uint32_t)i | (k & 0x80000000u);
+}
+
+__global__ void k_iota(uint32_t *a, size_t n) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) a[i] = (uint32_t)i;
+}
+
+// one lane per bucket, buckets visited in descending-size order
+template <int G>
+__global__ void __launch_bounds__(256) k_accumulate(const uint32_t *__restrict__ order, const uint32_t *__restrict__ counts,
+                                                    const uint32_t *__restrict__ offsets,
+                                                    const uint32_t *__restrict__ sorted,
+                                                    const Aff<typename FieldOf<G>::F> *__restrict__ pts,
+                                                    Xyzz<typename FieldOf<G>::F> *__restrict__ buckets, size_t nbuckets) {
+  typedef typename FieldOf<G>::F F;
+  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nbuckets) return;
+  uint32_t id = order[t];
+  uint32_t cnt = counts[id], off = offsets[id];
+  Xyzz<F> acc;
+  xyzz_set_inf(acc);
+  for (uint32_t k = 0; k < cnt; ++k) {
+    uint32_t e = sorted[off + k];
+    Aff<F> p = ld16(&pts[e & 0x7fffffffu]);
+    if (f_is_zero_exact(p.x) && f_is_zero_exact(p.y)) continue;  // affine infinity (ec_ops.h:717)
+    xyzz_madd(acc, p, (e >> 31) != 0);
+  }
+  st16(&buckets[id], acc);
+}
+
+// One level of the bucket reduction.  Invariant per window:
+//   Total = sum_s Y_s + sum_s s * A_s,  s in [0, S)
+// Thread (w, s2) folds s = s2*L + j, j in [0, L):
+//   a = sum_j A_j,  r = sum_j j A_j (running sums),  Y' = sum_j Y_j + r,  A' = L * a
+// First level: A_s = bucket s+1 and Y_s = A_s (sum_b b B_b = sum_s (s+1) A_s).
+template <int G>
+__global__ void __launch_bounds__(256) k_reduce(const Xyzz<typename FieldOf<G>::F> *__restrict__ A,
+                                                const Xyzz<typename FieldOf<G>::F> *__restrict__ Y,
+                                                Xyzz<typename FieldOf<G>::F> *__restrict__ A2,
+                                                Xyzz<typename FieldOf<G>::F> *__restrict__ Y2, int S, int L,
+                                                int log2L, int W) {
+  typedef typename FieldOf<G>::F F;
+  int S2 = S / L;
+  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (size_t)W * S2) return;
+  size_t w = t / S2, s2 = t - w * S2;
+  const Xyzz<F> *Aw = A + w * S + s2 * L;
+  Xyzz<F> acc, r, y;
+  xyzz_set_inf(acc);
+  xyzz_set_inf(r);
+  for (int j = L - 1; j >= 1; --j) {
+    Xyzz<F> a = ld16(&Aw[j]);
+    xyzz_add(acc, a);
+    xyzz_add(r, acc);
+  }
+  Xyzz<F> a0 = ld16(&Aw[0]);
+  xyzz_add(acc, a0);
+  if (Y == nullptr) {
+    y = acc;
+  } else {
+    const Xyzz<F> *Yw = Y + w * S + s2 * L;
+    y = ld16(&Yw[0]);
+    for (int j = 1; j < L; ++j) {
+      Xyzz<F> v = ld16(&Yw[j]);
+      xyzz_add(y, v);
+    }
+  }
+  xyzz_add(y, r);
+  for (int k = 0; k < log2L; ++k) {
+    Xyzz<F> tmp = acc;
+    xyzz_dbl(acc, tmp);
+  }
+  st16(&A2[w * S2 + s2], acc);
+  st16(&Y2[w * S2 + s2], y);
+}
+
+// xyzz -> blst Jacobian (X*ZZ, Y*ZZZ, ZZ)  (ref ec_ops.h:771-777), canonical blst Montgomery
+template <int G>
+__global__ void k_finalize(const Xyzz<typename FieldOf<G>::F> *__restrict__ T, uint64_t *__restrict__ out, int W) {
+  typedef typename FieldOf<G>::F F;
+  int w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= W) return;
+  Xyzz<F> a = ld16(&T[w]);
+  F X, Y;
+  f_mul(X, a.x, a.zz);
+  f_mul(Y, a.y, a.zzz);
+  uint64_t *o = out + (size_t)w * 18 * G;
+  if (xyzz_is_inf(a)) {
+    for (int k = 0; k < 18 * G; ++k) o[k] = 0;
+    return;
+  }
+  f_to_blst(o, X);
+  f_to_blst(o + 6 * G, Y);
+  f_to_blst(o + 12 * G, a.zz);
+}
+
+}  // namespace msm
