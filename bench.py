@@ -1,0 +1,231 @@
+#!/usr/bin/env python3
+"""bench.py -- G1 MSM point-scalar pairs/s at n=2^20 per MI355X (BASELINE.json metric).
+
+One step = one complete G1 MSM over this rank's 2^20 fixed points with fresh
+scalars already resident in HBM (digits -> sort -> bucket accumulation ->
+bucket reduction -> window combine), plus, for N > 1, the single exchange of
+the partial sums (all_gather of 144-B Jacobians over RCCL) and their fold.
+Weak scaling: every GPU owns its own 2^20-point shard of the sequence
+P_i = 2^(i+1) G, so the job computes an MSM of N * 2^20 pairs per step.
+
+Usage:
+  python bench.py [--gpus N --steps K --warmup W]                 (N = 1)
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Prints ONE JSON line on rank 0 with value = total pairs / (max-over-ranks
+time of K steps), a `roofline` object for the dominant kernel (bucket
+accumulation, timed with HIP events on the stream it runs on), and a
+`cpu_baseline` object (the CPU oracle port of the reference's blst Pippenger,
+1 thread, on a bounded prefix of the same workload; rank 0, N = 1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "G1 MSM point-scalar pairs/sec at n=2^20, 1/2/4/8 MI355X; bit-exact vs CPU"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
+VALU_PEAK_LANE_OPS = 78.6e12   # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (one VALU op / lane / clk)
+MADS_PER_FPMUL = 392           # 14x14 product + 14x14 reduction, one v_mad_u64_u32 each (fp.hpp)
+BYTES_PER_PAIR = 128           # 96 B affine point + 32 B scalar (SURVEY 8d, G1 plain)
+FPMUL_PER_MADD = 10            # 8M + 2S (ec_ops.h:727-748)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--log-n", type=int, default=20, help="points per GPU = 2^log_n")
+    ap.add_argument("--window", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-log-n", type=int, default=20)
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+
+    import torch
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from msm_blst_amd import _ffi
+    if not os.path.exists(_ffi.LIB_PATH):
+        from msm_blst_amd import build
+        build.build()
+    import msm_blst_amd as m
+    from msm_blst_amd import dist as mdist
+
+    n = 1 << args.log_n
+    t0 = time.time()
+    start, _ = mdist.shard_range(n * world, world, rank)
+    pts = m.fixed_points(1, n, start)
+    sc = m.gen_scalars(n, 1 + rank)
+    log(f"[rank {rank}] inputs generated in {time.time() - t0:.1f}s (points {start}..{start + n})")
+
+    ctx = m.MSMContext(1, local, args.window)
+    stream = torch.cuda.current_stream(dev)
+    ctx.set_points(pts, n, stream=stream.cuda_stream)
+    d_sc = torch.frombuffer(bytearray(bytes(sc)), dtype=torch.uint8).to(dev)
+    torch.cuda.synchronize(dev)
+    ctx.set_profiling(True)
+
+    add = mdist.engine_add(1)
+
+    def step():
+        part = ctx.mult(d_sc.data_ptr(), 255, stride=32, on_device=True, stream=stream.cuda_stream)
+        if world > 1:
+            return mdist.fold(mdist.gather_partials(part, 1, dev), add)
+        return part
+
+    for _ in range(args.warmup):
+        res = step()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize(dev)
+    acc_ms, tot_ms = [], []
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+        ph = ctx.phase_times()
+        acc_ms.append(ph["accumulate"])
+        tot_ms.append(ph["total"])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    phases = ctx.phase_times()
+
+    # parity of the timed result (N = 1: the reference's golden value for seed 1)
+    parity = None
+    if world == 1 and args.log_n == 20:
+        gold = json.load(open(os.path.join(REPO, "tests", "golden", "msm_g1.json")))
+        want = [c for c in gold["cases"] if c["n"] == n and c["seed"] == 1 and c["case"] == "rand"][0]["compressed"]
+        parity = m.compress(1, res).hex() == want
+
+    if rank != 0:
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
+
+    total_pairs = n * world * args.steps
+    value = total_pairs / elapsed
+    W = (255 + 1 + args.window - 1) // args.window
+    acc_s = sum(acc_ms) / len(acc_ms) / 1e3
+    achieved_gbs = n * BYTES_PER_PAIR / acc_s / 1e9
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            traffic = json.load(open(args.traffic_json)).get("accumulate_bytes_per_launch")
+        except Exception:
+            traffic = None
+    fpmul_rate = n * W * FPMUL_PER_MADD / acc_s
+    fpmul_peak = VALU_PEAK_LANE_OPS / MADS_PER_FPMUL
+
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(m, pts, sc, args.cpu_sample_log_n, ctx_window=args.window)
+
+    line = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "pairs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32 (exact Fp381 integer arithmetic, 14x28-bit limbs)",
+        "data": "synthetic: P_i = 2^(i+1) G1 (main_p1.cpp:52-66), SplitMix64 scalars < r (BASELINE.md sec.3)",
+        "config": {"workload": f"G1 MSM n=2^{args.log_n} per GPU, plain Pippenger c={args.window} "
+                               f"({W} windows), points+scalars resident in HBM",
+                   "n_per_gpu": n, "n_total": n * world, "method": "pippenger", "window_bits": args.window,
+                   "parallelism": f"points sharded x{world}, RCCL all_gather of partials"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved_gbs / HBM_PEAK_GBS, 5), "traffic": traffic,
+                     "kernel": "k_accumulate (bucket accumulation)",
+                     "kernel_ms": round(acc_s * 1e3, 4),
+                     "algorithmic_bytes_per_launch": n * BYTES_PER_PAIR,
+                     "note": "kernel is VALU-integer bound, see valu_roofline"},
+        "valu_roofline": {"bound": "valu-int", "achieved": round(fpmul_rate / 1e9, 2),
+                          "peak": round(fpmul_peak / 1e9, 2), "unit": "G Fp-mul/s",
+                          "frac": round(fpmul_rate / fpmul_peak, 4),
+                          "work": f"{W} windows x 10 Fp-mul per madd per pair",
+                          "peak_basis": "78.6T VALU lane-ops/s / 392 v_mad_u64_u32 per Fp-mul"},
+        "phases_ms": {k: round(v, 4) for k, v in phases.items()},
+        "parity_vs_reference": parity,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+def cpu_baseline(m, pts, sc, log_n, ctx_window):
+    """The reference's own blst_p1s_mult_pippenger (libblst built from /root/reference
+    sources into oracle/_ref/libblst_ref.so, x86-64 mulx asm), 1 thread -- the
+    reference has no threading -- timed on this host's cores on the same points and
+    scalars; falls back to the oracle port (oracle/msm_oracle.c) if the reference
+    build is absent.  The result is cross-checked against the GPU result."""
+    import ctypes
+    k = 1 << log_n
+    P = (ctypes.c_uint8 * (96 * k)).from_buffer_copy(bytes(pts)[:96 * k])
+    S = (ctypes.c_uint8 * (32 * k)).from_buffer_copy(bytes(sc)[:32 * k])
+    ref_so = os.path.join(REPO, "oracle", "_ref", "libblst_ref.so")
+    if os.path.exists(ref_so):
+        R = ctypes.CDLL(ref_so)
+        R.blst_p1s_mult_pippenger_scratch_sizeof.restype = ctypes.c_size_t
+        R.blst_p1s_mult_pippenger_scratch_sizeof.argtypes = [ctypes.c_size_t]
+        R.blst_p1s_mult_pippenger.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_void_p, ctypes.c_size_t,
+                                                                        ctypes.c_void_p]
+        R.blst_p1s_mult_pippenger.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                              ctypes.c_size_t, ctypes.c_void_p]
+        scratch = (ctypes.c_uint8 * R.blst_p1s_mult_pippenger_scratch_sizeof(k))()
+        pp = (ctypes.c_void_p * 2)(ctypes.cast(P, ctypes.c_void_p), None)
+        sp = (ctypes.c_void_p * 2)(ctypes.cast(S, ctypes.c_void_p), None)
+        r = (ctypes.c_uint8 * 144)()
+        t = time.perf_counter()
+        R.blst_p1s_mult_pippenger(r, pp, k, sp, 255, scratch)
+        dt = time.perf_counter() - t
+        out = (ctypes.c_uint8 * 48)()
+        R.blst_p1_compress(out, r)
+        cpu_res, kind, what = bytes(out).hex(), "reference", "reference libblst blst_p1s_mult_pippenger (oracle/_ref)"
+    else:
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        import oracle_ffi as of
+        t = time.perf_counter()
+        r = of.msm(1, P, S, k, 255, "pippenger")
+        dt = time.perf_counter() - t
+        cpu_res, kind, what = of.compress(1, r), "port", "oracle port of blst Pippenger (oracle/msm_oracle.c)"
+    ctx = m.MSMContext(1, 0, ctx_window)
+    ctx.set_points(P, k)
+    gpu_res = m.compress(1, ctx.mult(S, 255)).hex()
+    ctx.close()
+    return {"value": round(k / dt, 1), "unit": "pairs/s", "cores": 1, "kind": kind,
+            "sample": f"{what}, 1 thread, first 2^{log_n} points/scalars of the rank-0 workload, {dt:.1f}s",
+            "matches_gpu": cpu_res == gpu_res}
+
+
+if __name__ == "__main__":
+    main()

@@ -90,6 +90,9 @@ void msm_ctx_destroy(msm_ctx *ctx);
 void msm_gen_scalars(byte *out32, size_t n, uint64_t seed);         /* BASELINE.md sec.3 SplitMix64 */
 void msm_p1_fixed_points(blst_p1_affine *out, size_t n);            /* P_i = 2^(i+1) G1 (main_p1.cpp:52-66) */
 void msm_p2_fixed_points(blst_p2_affine *out, size_t n);
+/* P_{start+i} = 2^(start+i+1) G for i < n: the shard of the same point sequence */
+void msm_p1_fixed_points_range(blst_p1_affine *out, size_t start, size_t n);
+void msm_p2_fixed_points_range(blst_p2_affine *out, size_t start, size_t n);
 void msm_p1_to_affine(blst_p1_affine *out, const blst_p1 *in);      /* e1.c:80-92 */
 void msm_p2_to_affine(blst_p2_affine *out, const blst_p2 *in);
 void msm_p1_compress(byte out[48], const blst_p1 *in);              /* e1.c:225-234 */

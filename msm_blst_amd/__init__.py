@@ -38,10 +38,10 @@ def gen_scalars(n, seed):
     return out
 
 
-def fixed_points(group, n):
-    """P_i = 2^(i+1) G (ref main_p1.cpp:52-66), blst affine layout."""
+def fixed_points(group, n, start=0):
+    """P_i = 2^(i+1) G for i in [start, start+n) (ref main_p1.cpp:52-66), blst affine layout."""
     out = (ctypes.c_uint8 * (POINT_BYTES[group] * n))()
-    getattr(lib(), f"msm_p{group}_fixed_points")(out, n)
+    getattr(lib(), f"msm_p{group}_fixed_points_range")(out, start, n)
     return out
 
 

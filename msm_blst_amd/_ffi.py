@@ -35,8 +35,8 @@ def lib():
         f = getattr(L, f"blst_p{g}s_mult_pippenger_scratch_sizeof")
         f.argtypes = [sz]
         f.restype = sz
-        for name in (f"msm_p{g}_fixed_points",):
-            getattr(L, name).argtypes = [vp, sz]
+        getattr(L, f"msm_p{g}_fixed_points").argtypes = [vp, sz]
+        getattr(L, f"msm_p{g}_fixed_points_range").argtypes = [vp, sz, sz]
         for name in (f"msm_p{g}_to_affine", f"msm_p{g}_compress"):
             getattr(L, name).argtypes = [vp, vp]
         getattr(L, f"msm_p{g}_add").argtypes = [vp, vp, vp]

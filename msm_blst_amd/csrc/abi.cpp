@@ -323,11 +323,17 @@ void msm_gen_scalars(byte *out, size_t n, uint64_t seed) {
   }
 }
 
-void msm_p1_fixed_points(blst_p1_affine *out, size_t n) {
-  fixed_points<hfp::Fp>(reinterpret_cast<hfp::Aff<hfp::Fp> *>(out), n, hfp::g1_generator());
+void msm_p1_fixed_points(blst_p1_affine *out, size_t n) { msm_p1_fixed_points_range(out, 0, n); }
+void msm_p2_fixed_points(blst_p2_affine *out, size_t n) { msm_p2_fixed_points_range(out, 0, n); }
+void msm_p1_fixed_points_range(blst_p1_affine *out, size_t start, size_t n) {
+  hfp::Jac<hfp::Fp> g = hfp::g1_generator();
+  for (size_t i = 0; i < start; ++i) g = hfp::dbl(g);
+  fixed_points<hfp::Fp>(reinterpret_cast<hfp::Aff<hfp::Fp> *>(out), n, g);
 }
-void msm_p2_fixed_points(blst_p2_affine *out, size_t n) {
-  fixed_points<hfp::Fp2>(reinterpret_cast<hfp::Aff<hfp::Fp2> *>(out), n, hfp::g2_generator());
+void msm_p2_fixed_points_range(blst_p2_affine *out, size_t start, size_t n) {
+  hfp::Jac<hfp::Fp2> g = hfp::g2_generator();
+  for (size_t i = 0; i < start; ++i) g = hfp::dbl(g);
+  fixed_points<hfp::Fp2>(reinterpret_cast<hfp::Aff<hfp::Fp2> *>(out), n, g);
 }
 void msm_p1_to_affine(blst_p1_affine *out, const blst_p1 *in) {
   *reinterpret_cast<hfp::Aff<hfp::Fp> *>(out) = hfp::to_affine(*reinterpret_cast<const hfp::Jac<hfp::Fp> *>(in));
