@@ -86,6 +86,44 @@ int msm_ctx_set_profiling(msm_ctx *ctx, int on);
 int msm_ctx_phase_times(const msm_ctx *ctx, float out[6]);
 void msm_ctx_destroy(msm_ctx *ctx);
 
+/* ---- CHES "nh + q/5" bucket-set method, device-resident precomputed table ----
+ * Replaces the driver-level CHES path of ref main_p1.cpp: init_pippenger_CHES_q_over_5
+ * (:128-178: bucket set, digit hash, table T[3(i h + j) + m - 1] = m q^j P_i) and
+ * pippenger_variant_q_over_5_CHES (:192-246: MB digit conversion, accumulation
+ * blst_p1_tile_pippenger_d_CHES, reduction :301-321).  The table is built on
+ * the GPU (or uploaded) once; each mult takes n 32-byte scalars.  The result is
+ * the true sum_i s_i P_i (the reference's last-element guard defect,
+ * multi_scalar.c:461, is not reproduced; scalars >= r are reduced mod r where
+ * the reference requires s < r). */
+typedef struct msm_ches_ctx msm_ches_ctx;
+/* the configuration of ref ches_config_files/config_file_n_exp_<n_exp>[_beta].h:
+ * out = {n_exp, beta, q_exp, h, a_h, d_max, b_size, q_exp_bgmw, h_bgmw} */
+int msm_ches_params(int n_exp, int beta, int out[9]);
+int msm_ches_ctx_create(msm_ches_ctx **ctx, int group, int device, int n_exp, int beta);
+/* explicit parameters (same 9-int layout; b_size 0 = not checked) */
+int msm_ches_ctx_create_params(msm_ches_ctx **ctx, int group, int device, const int params[9]);
+/* base points P_i (blst affine) -> T built on the GPU */
+int msm_ches_ctx_build_table(msm_ches_ctx *ctx, const void *points_affine, size_t npoints, int on_device,
+                             void *hip_stream);
+/* a precomputed T (blst affine, 3 * npoints * h entries, main_p1.cpp:155-172 order) */
+int msm_ches_ctx_set_table(msm_ches_ctx *ctx, const void *table_affine, size_t npoints, int on_device,
+                           void *hip_stream);
+/* T[first, first + count) in blst affine layout, to host memory */
+int msm_ches_ctx_get_table(msm_ches_ctx *ctx, void *out_affine, size_t first, size_t count);
+/* scalars: npoints 32-byte LE strings with the given stride (>= 32), host or device */
+int msm_ches_ctx_mult(msm_ches_ctx *ctx, void *ret, const byte *scalars, size_t stride, int scalars_on_device,
+                      void *hip_stream);
+int msm_ches_ctx_set_profiling(msm_ches_ctx *ctx, int on);
+int msm_ches_ctx_phase_times(const msm_ches_ctx *ctx, float out[6]);
+size_t msm_ches_ctx_bucket_count(const msm_ches_ctx *ctx);
+void msm_ches_ctx_destroy(msm_ches_ctx *ctx);
+
+/* host setup logic of the CHES method (no device work):
+ * bucket set of ref auxiliaryfunc.h:257-288 (returns |B|; out may be NULL) */
+size_t msm_ches_bucket_set(int q, int a_h, int *out, size_t cap);
+/* digit hash of ref main_p1.cpp:140-152, q+1 entries in the blst.h:253 layout */
+int msm_ches_digit_table(int q, int a_h, digit_decomposition *out);
+
 /* ---- boundary helpers (host; no blst symbols are redefined) ---- */
 void msm_gen_scalars(byte *out32, size_t n, uint64_t seed);         /* BASELINE.md sec.3 SplitMix64 */
 void msm_p1_fixed_points(blst_p1_affine *out, size_t n);            /* P_i = 2^(i+1) G1 (main_p1.cpp:52-66) */

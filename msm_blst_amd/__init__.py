@@ -13,8 +13,9 @@ Mirrors:
 import ctypes
 
 from ._ffi import MsmError, check, lib
+from .ches import CHESContext
 
-__all__ = ["MsmError", "MSMContext", "p1s_mult_pippenger", "p2s_mult_pippenger", "fixed_points", "gen_scalars",
+__all__ = ["MsmError", "MSMContext", "CHESContext", "p1s_mult_pippenger", "p2s_mult_pippenger", "fixed_points", "gen_scalars",
            "compress", "to_affine", "device_count", "lib"]
 
 POINT_BYTES = {1: 96, 2: 192}

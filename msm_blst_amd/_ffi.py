@@ -52,9 +52,23 @@ def lib():
     L.msm_gen_scalars.argtypes = [vp, sz, u64]
     L.msm_test_field.argtypes = [i32, i32, vp, vp, vp, sz]
     L.msm_test_xyzz.argtypes = [i32, vp, sz, vp, i32, sz, vp]
-    for name in ("msm_ches_ctx_create",):
-        if hasattr(L, name):
-            pass
+    pp = ctypes.POINTER(vp)
+    L.msm_ches_params.argtypes = [i32, i32, vp]
+    L.msm_ches_ctx_create.argtypes = [pp, i32, i32, i32, i32]
+    L.msm_ches_ctx_create_params.argtypes = [pp, i32, i32, vp]
+    L.msm_ches_ctx_build_table.argtypes = [vp, vp, sz, i32, vp]
+    L.msm_ches_ctx_set_table.argtypes = [vp, vp, sz, i32, vp]
+    L.msm_ches_ctx_get_table.argtypes = [vp, vp, sz, sz]
+    L.msm_ches_ctx_mult.argtypes = [vp, vp, vp, sz, i32, vp]
+    L.msm_ches_ctx_set_profiling.argtypes = [vp, i32]
+    L.msm_ches_ctx_phase_times.argtypes = [vp, vp]
+    L.msm_ches_ctx_bucket_count.argtypes = [vp]
+    L.msm_ches_ctx_bucket_count.restype = sz
+    L.msm_ches_ctx_destroy.argtypes = [vp]
+    L.msm_ches_ctx_destroy.restype = None
+    L.msm_ches_bucket_set.argtypes = [i32, i32, vp, sz]
+    L.msm_ches_bucket_set.restype = sz
+    L.msm_ches_digit_table.argtypes = [i32, i32, vp]
     _lib = L
     return L
 

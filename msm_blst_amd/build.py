@@ -20,7 +20,9 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("MSM_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-value",
          "-Wno-unused-function", f"-I{os.path.join(REPO, 'include')}"]
-SOURCES = ["engine.hip", "ches.hip", "abi.cpp"]
+# (source, MSM_GROUP or None): the group-templated engines compile once per
+# group in parallel (the G2 instantiations dominate the build time)
+SOURCES = [("engine.hip", 1), ("engine.hip", 2), ("ches.hip", 1), ("ches.hip", 2), ("abi.cpp", None)]
 
 
 def _deps():
@@ -34,19 +36,21 @@ def _stale(target, inputs):
     return any(os.path.getmtime(i) > t for i in inputs if os.path.exists(i))
 
 
-def build(verbose=False, jobs=4):
+def build(verbose=False, jobs=5):
     os.makedirs(OBJ, exist_ok=True)
     hdrs = _deps()
     jobs_list = []
     objs = []
-    for src in SOURCES:
+    for src, grp in SOURCES:
         sp = os.path.join(CSRC, src)
         if not os.path.exists(sp):
             continue
-        op = os.path.join(OBJ, os.path.splitext(src)[0] + ".o")
+        stem = os.path.splitext(src)[0] + (f"_g{grp}" if grp else "")
+        op = os.path.join(OBJ, stem + ".o")
         objs.append(op)
         if _stale(op, [sp] + hdrs):
-            jobs_list.append([HIPCC] + FLAGS + ["-c", sp, "-o", op])
+            defs = [f"-DMSM_GROUP={grp}"] if grp else []
+            jobs_list.append([HIPCC] + FLAGS + defs + ["-c", sp, "-o", op])
 
     def run(cmd):
         if verbose:

@@ -9,6 +9,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -159,6 +160,14 @@ void fixed_points(hfp::Aff<F> *out, size_t n, hfp::Jac<F> g) {
   hfp::to_affine_batch(out, j.data(), n);
 }
 
+struct msm_ches_ctx {
+  int group = 1;
+  int device = 0;
+  std::unique_ptr<Ches<1>> g1;
+  std::unique_ptr<Ches<2>> g2;
+  DevBuf scalars;
+};
+
 struct msm_ctx {
   int group = 1;
   int device = 0;
@@ -293,6 +302,140 @@ int msm_ctx_phase_times(const msm_ctx *ctx, float out[6]) {
 }
 
 void msm_ctx_destroy(msm_ctx *ctx) { delete ctx; }
+
+// ---------------- CHES contexts ----------------
+static void params_out(const ChesParams &p, int out[9]) {
+  const int v[9] = {p.n_exp, p.beta, p.q_exp, p.h, p.a_h, p.d_max, p.b_size, p.q_exp_bgmw, p.h_bgmw};
+  memcpy(out, v, sizeof v);
+}
+
+int msm_ches_params(int n_exp, int beta, int out[9]) {
+  ChesParams p;
+  if (!out || !ches_params_for(n_exp, beta, &p)) return fail(MSM_E_ARG, "no CHES configuration for n_exp/beta");
+  params_out(p, out);
+  return MSM_OK;
+}
+
+int msm_ches_ctx_create_params(msm_ches_ctx **ctx, int group, int device, const int v[9]) {
+  if (!ctx || !v || (group != 1 && group != 2)) return fail(MSM_E_ARG, "bad ctx/group/params");
+  if (msm_device_count() <= device || device < 0) return fail(MSM_E_NODEV, "no such HIP device");
+  ChesParams p{v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], v[8]};
+  try {
+    auto c = std::make_unique<msm_ches_ctx>();
+    c->group = group;
+    c->device = device;
+    if (group == 1) c->g1 = std::make_unique<Ches<1>>(device, p);
+    else c->g2 = std::make_unique<Ches<2>>(device, p);
+    *ctx = c.release();
+    return MSM_OK;
+  } catch (const std::exception &e) {
+    return fail(MSM_E_HIP, e.what());
+  }
+}
+
+int msm_ches_ctx_create(msm_ches_ctx **ctx, int group, int device, int n_exp, int beta) {
+  int v[9];
+  int rc = msm_ches_params(n_exp, beta, v);
+  if (rc) return rc;
+  return msm_ches_ctx_create_params(ctx, group, device, v);
+}
+
+#define CHES_DISPATCH(ctx, CALL) ((ctx)->group == 1 ? (ctx)->g1->CALL : (ctx)->g2->CALL)
+
+int msm_ches_ctx_build_table(msm_ches_ctx *ctx, const void *pts, size_t n, int on_device, void *stream) {
+  if (!ctx || (!pts && n)) return fail(MSM_E_ARG, "bad args");
+  try {
+    CHES_DISPATCH(ctx, build_table(pts, n, on_device != 0, (hipStream_t)stream));
+    return MSM_OK;
+  } catch (const std::exception &e) {
+    return fail(MSM_E_HIP, e.what());
+  }
+}
+
+int msm_ches_ctx_set_table(msm_ches_ctx *ctx, const void *tab, size_t n, int on_device, void *stream) {
+  if (!ctx || (!tab && n)) return fail(MSM_E_ARG, "bad args");
+  try {
+    CHES_DISPATCH(ctx, set_table(tab, n, on_device != 0, (hipStream_t)stream));
+    return MSM_OK;
+  } catch (const std::exception &e) {
+    return fail(MSM_E_HIP, e.what());
+  }
+}
+
+int msm_ches_ctx_get_table(msm_ches_ctx *ctx, void *out, size_t first, size_t count) {
+  if (!ctx || (!out && count)) return fail(MSM_E_ARG, "bad args");
+  try {
+    CHES_DISPATCH(ctx, get_table(out, first, count, (hipStream_t)0));
+    return MSM_OK;
+  } catch (const std::exception &e) {
+    return fail(MSM_E_HIP, e.what());
+  }
+}
+
+int msm_ches_ctx_mult(msm_ches_ctx *ctx, void *ret, const byte *scalars, size_t stride, int on_device,
+                      void *stream) {
+  if (!ctx || !ret || stride < 32) return fail(MSM_E_ARG, "bad args (stride must be >= 32)");
+  try {
+    DeviceGuard g(ctx->device);
+    hipStream_t s = (hipStream_t)stream;
+    size_t n = CHES_DISPATCH(ctx, npoints());
+    const uint8_t *d = scalars;
+    if (!on_device && n) {
+      ctx->scalars.ensure(n * stride + 16);
+      MSM_HIP_CHECK(hipMemcpyAsync(ctx->scalars.p, scalars, n * stride, hipMemcpyHostToDevice, s));
+      d = ctx->scalars.as<uint8_t>();
+    }
+    if (ctx->group == 1) {
+      hfp::Jac<hfp::Fp> out;
+      ctx->g1->run(s, d, stride, &out);
+      memcpy(ret, &out, sizeof out);
+    } else {
+      hfp::Jac<hfp::Fp2> out;
+      ctx->g2->run(s, d, stride, &out);
+      memcpy(ret, &out, sizeof out);
+    }
+    return MSM_OK;
+  } catch (const std::exception &e) {
+    return fail(MSM_E_HIP, e.what());
+  }
+}
+
+int msm_ches_ctx_set_profiling(msm_ches_ctx *ctx, int on) {
+  if (!ctx) return fail(MSM_E_ARG, "null ctx");
+  CHES_DISPATCH(ctx, set_profiling(on != 0));
+  return MSM_OK;
+}
+
+int msm_ches_ctx_phase_times(const msm_ches_ctx *ctx, float out[6]) {
+  if (!ctx || !out) return fail(MSM_E_ARG, "null");
+  const PhaseTimes &t = CHES_DISPATCH(ctx, times());
+  const float v[6] = {t.digits, t.sort, t.accumulate, t.reduce, t.finalize, t.total};
+  memcpy(out, v, sizeof v);
+  return MSM_OK;
+}
+
+size_t msm_ches_ctx_bucket_count(const msm_ches_ctx *ctx) { return ctx ? CHES_DISPATCH(ctx, bucket_count()) : 0; }
+
+void msm_ches_ctx_destroy(msm_ches_ctx *ctx) { delete ctx; }
+
+size_t msm_ches_bucket_set(int q, int a_h, int *out, size_t cap) {
+  if (q < 4 || a_h < 0) return 0;
+  std::vector<int> B = ches_bucket_set(q, a_h);
+  if (out) memcpy(out, B.data(), std::min(cap, B.size()) * sizeof(int));
+  return B.size();
+}
+
+int msm_ches_digit_table(int q, int a_h, digit_decomposition *out) {
+  if (q < 4 || a_h < 0 || !out) return fail(MSM_E_ARG, "bad args");
+  std::vector<int> B = ches_bucket_set(q, a_h);
+  std::vector<uint32_t> H = ches_digit_hash(B, q);
+  for (size_t d = 0; d < H.size(); ++d) {
+    out[d].m = (int)((H[d] >> 24) & 3u) + 1;
+    out[d].b = B[H[d] & 0x00ffffffu];
+    out[d].alpha = (int)(H[d] >> 31);
+  }
+  return MSM_OK;
+}
 
 // ---------------- boundary helpers ----------------
 static uint64_t splitmix64(uint64_t *s) {

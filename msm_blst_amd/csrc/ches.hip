@@ -1,1 +1,389 @@
-// ches.hip -- CHES bucket-set pipeline (filled in below)
+// ches.hip -- host orchestration of the CHES "nh + q/5" bucket-set MSM
+// (LuoGuiwen/MSM_blst, method `pippenger_variant_q_over_5_CHES`,
+// ref main_p1.cpp:192-246) on one MI355X.
+//
+// Setup (once per context): parameters of ref ches_config_files, bucket set B
+// (ref auxiliaryfunc.h:257-288), digit hash (ref main_p1.cpp:140-152) and the
+// precomputed table T[3(i h + j) + m - 1] = m q^j P_i (ref main_p1.cpp:155-172),
+// the latter built on the GPU and kept resident in HBM in the engine's
+// internal limb layout.
+//
+// Per MSM (all on device, one stream):
+//   digits   k_ches_digits: MB radix-q digits + per-bucket counts/ranks
+//   sort     exclusive scan of counts, k_ches_scatter, bucket schedule by size
+//   accum    k_accumulate: one lane per bucket, xyzz += +-T[slot]
+//   reduce   WeightedReducer: sum_i B[i] S_i (replaces the d-trick loop of
+//            ref multi_scalar.c:301-321 with a GPU-parallel regrouping)
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstring>
+
+#include "ches_kernels.hpp"
+#include "engine.hpp"
+
+#ifndef MSM_GROUP
+#error "define MSM_GROUP (1 or 2)"
+#endif
+
+namespace msm {
+
+#if MSM_GROUP == 1  // group-independent host setup: compiled once
+// ------------------------------------------------------------- parameters --
+// values of ref ches_config_files/config_file_n_exp_{8..21}.h and the _beta
+// variants (n_exp, beta, q exponent, h, a_h, d_max, |B|, BGMW95 q exponent, h)
+static const ChesParams kChesTable[] = {
+    {8, 0, 12, 22, 7, 6, 857, 10, 26},         {9, 0, 13, 20, 231, 6, 1725, 11, 24},
+    {10, 0, 13, 20, 231, 6, 1725, 12, 22},     {11, 0, 14, 19, 7, 6, 3417, 13, 20},
+    {12, 0, 14, 19, 7, 6, 3417, 13, 20},       {13, 0, 16, 16, 29677, 6, 18343, 15, 17},
+    {14, 0, 16, 16, 29677, 6, 18343, 15, 17},  {15, 0, 16, 16, 29677, 6, 18343, 16, 16},
+    {16, 0, 19, 14, 231, 6, 109244, 17, 15},   {16, 1, 18, 15, 7, 6, 54618, 17, 15},
+    {17, 0, 20, 13, 29677, 6, 220931, 17, 15}, {17, 1, 19, 14, 231, 6, 109244, 17, 15},
+    {18, 0, 20, 13, 29677, 6, 220931, 19, 14}, {19, 0, 20, 13, 29677, 6, 220931, 20, 13},
+    {20, 0, 22, 12, 7419, 6, 874437, 20, 13},  {20, 1, 20, 13, 29677, 6, 220931, 20, 13},
+    {21, 0, 22, 12, 7419, 6, 874437, 22, 12},
+};
+
+bool ches_params_for(int n_exp, int beta, ChesParams *out) {
+  for (const ChesParams &p : kChesTable)
+    if (p.n_exp == n_exp && p.beta == beta) {
+      *out = p;
+      return true;
+    }
+  return false;
+}
+
+// omega2(v) + omega3(v) even  (ref auxiliaryfunc.h:217-255)
+static bool even23(int v) {
+  int e = 0;
+  while (v % 2 == 0) v /= 2, ++e;
+  while (v % 3 == 0) v /= 3, ++e;
+  return (e & 1) == 0;
+}
+
+// ref auxiliaryfunc.h:257-288: {0,1} u {i <= q/2 : even23(i)}, then the two
+// pruning passes (membership tested as the passes run, as std::set::erase
+// does there), then every even23 value <= a_h + 1 re-inserted.
+std::vector<int> ches_bucket_set(int q, int a_h) {
+  size_t lim = std::max<size_t>((size_t)q / 2 + 1, (size_t)a_h + 2);
+  std::vector<uint8_t> in(lim, 0);
+  in[0] = in[1] = 1;
+  for (int i = 2; i <= q / 2; ++i) in[i] = even23(i);
+  for (int i = q / 4; i < q / 2; ++i) {
+    int t = q - 2 * i;
+    if (in[i] && t >= 0 && (size_t)t < lim && in[t]) in[t] = 0;
+  }
+  for (int i = q / 6; i < q / 4; ++i) {
+    int t = q - 3 * i;
+    if (in[i] && t >= 0 && (size_t)t < lim && in[t]) in[t] = 0;
+  }
+  for (int i = 1; i <= a_h + 1; ++i)
+    if (even23(i)) in[i] = 1;
+  std::vector<int> B;
+  for (size_t v = 0; v < lim; ++v)
+    if (in[v]) B.push_back((int)v);
+  return B;
+}
+
+// ref main_p1.cpp:140-152: every (m, b) writes H[q - m b] = (m, b, alpha=1),
+// then H[m b] = (m, b, 0); later writes win.  Packed per ches_kernels.hpp.
+std::vector<uint32_t> ches_digit_hash(const std::vector<int> &B, int q) {
+  std::vector<uint32_t> H((size_t)q + 1, 0);
+  for (int alpha = 1; alpha >= 0; --alpha)
+    for (int m = 1; m <= 3; ++m)
+      for (size_t i = 0; i < B.size(); ++i) {
+        long mb = (long)m * B[i];
+        if (mb > q) continue;
+        size_t d = alpha ? (size_t)(q - mb) : (size_t)mb;
+        H[d] = (uint32_t)i | ((uint32_t)(m - 1) << 24) | ((uint32_t)alpha << 31);
+      }
+  return H;
+}
+#endif  // MSM_GROUP == 1
+
+// ---------------------------------------------------------- reduction plan --
+// sum_i B[i] S_i = sum_u u L_u + 2^s sum_v v H_v  with u = B[i] mod 2^s,
+// v = B[i] >> s, L_u = sum_{i: low(B[i]) = u} S_i, H_v = sum_{i: high(B[i]) = v} S_i.
+// L and H are segment sums over one list of 2(|B|-1) bucket indices (level 0:
+// chunks of <= 8 within a segment; then pairwise levels until one partial per
+// segment; then a dense scatter into 2 windows of 2^s slots), followed by the
+// dense 2-window reduction and a 2^s Horner step on the host.
+template <int G>
+void WeightedReducer<G>::plan(const std::vector<int> &B) {
+  typedef typename FieldOf<G>::F F;
+  bsize_ = B.size();
+  starts_.clear();
+  nout_.clear();
+  int maxB = B.empty() ? 0 : B.back();
+  for (size_t i = 1; i < B.size(); ++i)
+    if (B[i] <= B[i - 1]) throw std::runtime_error("bucket set must be strictly ascending");
+  if (!B.empty() && B[0] != 0) throw std::runtime_error("bucket set must start with 0");
+  int bits = 0;
+  while (bits < 31 && (1 << bits) <= maxB) ++bits;
+  sbits_ = std::max(1, (bits + 1) / 2);
+  const uint32_t S = 1u << sbits_;
+  std::vector<uint32_t> idx, seg;
+  for (size_t i = 1; i < B.size(); ++i) {  // high halves, ascending v
+    uint32_t v = (uint32_t)B[i] >> sbits_;
+    if (v) idx.push_back((uint32_t)i), seg.push_back(S + v - 1);
+  }
+  std::vector<std::vector<uint32_t>> byu(S);
+  for (size_t i = 1; i < B.size(); ++i) {
+    uint32_t u = (uint32_t)B[i] & (S - 1);
+    if (u) byu[u].push_back((uint32_t)i);
+  }
+  for (uint32_t u = 1; u < S; ++u)
+    for (uint32_t i : byu[u]) idx.push_back(i), seg.push_back(u - 1);
+  // level 0 + pairwise levels
+  std::vector<uint32_t> cur_seg = seg;
+  int C = 8;
+  while (true) {
+    std::vector<uint32_t> st, nseg;
+    size_t k = 0;
+    while (k < cur_seg.size()) {
+      st.push_back((uint32_t)k);
+      nseg.push_back(cur_seg[k]);
+      size_t e = k + 1;
+      while (e < cur_seg.size() && e - k < (size_t)C && cur_seg[e] == cur_seg[k]) ++e;
+      k = e;
+    }
+    st.push_back((uint32_t)cur_seg.size());
+    bool first = starts_.empty();
+    if (!first && nseg.size() == cur_seg.size()) break;  // nothing merged: one partial per segment
+    starts_.emplace_back();
+    starts_.back().ensure(st.size() * 4);
+    MSM_HIP_CHECK(hipMemcpy(starts_.back().p, st.data(), st.size() * 4, hipMemcpyHostToDevice));
+    nout_.push_back(nseg.size());
+    cur_seg.swap(nseg);
+    C = 2;
+    if (cur_seg.empty()) break;
+  }
+  // dense scatter: slot -> its single partial (or empty)
+  std::vector<uint32_t> dst(2 * S + 1, 0);
+  {
+    std::vector<int> at(2 * S, -1);
+    for (size_t k = 0; k < cur_seg.size(); ++k) at[cur_seg[k]] = (int)k;
+    // express as CSR over the partial array: ranges of length 0/1 need a permuted
+    // index, so the final level uses idx = perm with starts 0..count
+    std::vector<uint32_t> perm;
+    for (uint32_t sl = 0; sl < 2 * S; ++sl) {
+      dst[sl] = (uint32_t)perm.size();
+      if (at[sl] >= 0) perm.push_back((uint32_t)at[sl]);
+    }
+    dst[2 * S] = (uint32_t)perm.size();
+    starts_.emplace_back();
+    starts_.back().ensure(dst.size() * 4);
+    MSM_HIP_CHECK(hipMemcpy(starts_.back().p, dst.data(), dst.size() * 4, hipMemcpyHostToDevice));
+    nout_.push_back(2 * S);
+    // idx buffer: [level-0 item list | final permutation]
+    std::vector<uint32_t> all = idx;
+    all.insert(all.end(), perm.begin(), perm.end());
+    idx_.ensure(std::max<size_t>(all.size(), 1) * 4);
+    if (!all.empty()) MSM_HIP_CHECK(hipMemcpy(idx_.p, all.data(), all.size() * 4, hipMemcpyHostToDevice));
+    final_perm_off_ = idx.size();
+  }
+  size_t maxp = 1;
+  for (size_t l = 0; l + 1 < nout_.size(); ++l) maxp = std::max(maxp, nout_[l]);
+  part_[0].ensure(maxp * sizeof(Xyzz<F>));
+  part_[1].ensure(maxp * sizeof(Xyzz<F>));
+  dense_buf_.ensure((size_t)2 * S * sizeof(Xyzz<F>));
+}
+
+template <int G>
+void WeightedReducer<G>::launch(hipStream_t s, const void *Sbuf) {
+  typedef typename FieldOf<G>::F F;
+  const size_t L = nout_.size();
+  const Xyzz<F> *src = reinterpret_cast<const Xyzz<F> *>(Sbuf);
+  const uint32_t *idx = idx_.as<uint32_t>();
+  for (size_t l = 0; l < L; ++l) {
+    const bool last = l + 1 == L;
+    Xyzz<F> *dst = last ? dense_buf_.as<Xyzz<F>>() : part_[l & 1].as<Xyzz<F>>();
+    const uint32_t *ix = l == 0 ? idx : (last ? idx + final_perm_off_ : nullptr);
+    if (last && L == 1) src = reinterpret_cast<const Xyzz<F> *>(Sbuf);  // no items at all
+    if (nout_[l])
+      hipLaunchKernelGGL(k_segsum<G>, dim3(nblk(nout_[l], 64)), dim3(64), 0, s, src, ix, starts_[l].as<uint32_t>(),
+                         dst, nout_[l]);
+    MSM_HIP_CHECK(hipGetLastError());
+    src = dst;
+  }
+  dense_.launch(s, dense_buf_.p, 2, 1 << sbits_);
+}
+
+template <int G>
+hfp::Jac<typename HostField<G>::F> WeightedReducer<G>::read(hipStream_t s) {
+  std::vector<hfp::Jac<HF>> T;
+  dense_.read(s, 2, T);
+  return horner(T, sbits_);
+}
+
+template class WeightedReducer<MSM_GROUP>;
+
+// ------------------------------------------------------------------ Ches --
+template <int G>
+Ches<G>::Ches(int device, const ChesParams &p) : dev_(device), p_(p) {
+  DeviceGuard g(dev_);
+  if (p.q_exp < 2 || p.q_exp > 24 || p.h < 1 || p.h > 64 || (long)p.q_exp * p.h < 255)
+    throw std::runtime_error("bad CHES parameters");
+  const int q = 1 << p.q_exp;
+  B_ = ches_bucket_set(q, p.a_h);
+  if (p.b_size > 0 && (int)B_.size() != p.b_size)
+    throw std::runtime_error("bucket set size " + std::to_string(B_.size()) + " != configured " +
+                             std::to_string(p.b_size));
+  std::vector<uint32_t> H = ches_digit_hash(B_, q);
+  hash_.ensure(H.size() * 4);
+  MSM_HIP_CHECK(hipMemcpy(hash_.p, H.data(), H.size() * 4, hipMemcpyHostToDevice));
+  red_.plan(B_);
+  ev_.resize(8);
+  for (auto &e : ev_) MSM_HIP_CHECK(hipEventCreate(&e));
+}
+template <int G>
+Ches<G>::~Ches() {
+  for (auto &e : ev_) (void)hipEventDestroy(e);
+}
+
+template <int G>
+void Ches<G>::build_table(const void *pts, size_t n, bool on_device, hipStream_t s) {
+  typedef typename FieldOf<G>::F F;
+  DeviceGuard g(dev_);
+  const size_t K = 3 * (size_t)p_.h;
+  if (n == 0) {
+    n_ = 0;
+    return;
+  }
+  if (K * n >= (1ull << 31)) throw std::runtime_error("CHES table too large for 31-bit slots");
+  const size_t raw = n * 96 * G;
+  const void *src = pts;
+  DevBuf stage, base;
+  if (!on_device) {
+    stage.ensure(raw);
+    MSM_HIP_CHECK(hipMemcpyAsync(stage.p, pts, raw, hipMemcpyHostToDevice, s));
+    src = stage.p;
+  }
+  base.ensure(n * sizeof(Aff<F>));
+  hipLaunchKernelGGL(k_convert_points<G>, dim3(nblk(n, 256)), dim3(256), 0, s, (const uint64_t *)src,
+                     base.as<Aff<F>>(), n);
+  MSM_HIP_CHECK(hipGetLastError());
+  table_.ensure(K * n * sizeof(Aff<F>));
+  const size_t chunk = std::min<size_t>(n, (size_t)1 << 16);
+  DevBuf scratch, pref;
+  scratch.ensure(K * chunk * sizeof(Xyzz<F>));
+  pref.ensure(K * chunk * sizeof(F));
+  for (size_t i0 = 0; i0 < n; i0 += chunk) {
+    size_t cnt = std::min(chunk, n - i0);
+    hipLaunchKernelGGL(k_ches_table<G>, dim3(nblk(cnt, 64)), dim3(64), 0, s, base.as<Aff<F>>(), i0, cnt, p_.q_exp,
+                       p_.h, scratch.as<Xyzz<F>>(), pref.as<F>(), table_.as<Aff<F>>());
+    MSM_HIP_CHECK(hipGetLastError());
+  }
+  MSM_HIP_CHECK(hipStreamSynchronize(s));
+  n_ = n;
+}
+
+template <int G>
+void Ches<G>::set_table(const void *tab, size_t n, bool on_device, hipStream_t s) {
+  typedef typename FieldOf<G>::F F;
+  DeviceGuard g(dev_);
+  const size_t K = 3 * (size_t)p_.h, cnt = K * n;
+  if (cnt >= (1ull << 31)) throw std::runtime_error("CHES table too large for 31-bit slots");
+  const void *src = tab;
+  DevBuf stage;
+  if (!on_device && cnt) {
+    stage.ensure(cnt * 96 * G);
+    MSM_HIP_CHECK(hipMemcpyAsync(stage.p, tab, cnt * 96 * G, hipMemcpyHostToDevice, s));
+    src = stage.p;
+  }
+  table_.ensure(std::max<size_t>(cnt, 1) * sizeof(Aff<F>));
+  if (cnt)
+    hipLaunchKernelGGL(k_convert_points<G>, dim3(nblk(cnt, 256)), dim3(256), 0, s, (const uint64_t *)src,
+                       table_.as<Aff<F>>(), cnt);
+  MSM_HIP_CHECK(hipGetLastError());
+  MSM_HIP_CHECK(hipStreamSynchronize(s));
+  n_ = n;
+}
+
+template <int G>
+void Ches<G>::get_table(void *out, size_t first, size_t count, hipStream_t s) {
+  typedef typename FieldOf<G>::F F;
+  DeviceGuard g(dev_);
+  if (first + count > 3 * (size_t)p_.h * n_) throw std::runtime_error("table range out of bounds");
+  if (!count) return;
+  DevBuf o;
+  o.ensure(count * 96 * G);
+  hipLaunchKernelGGL(k_export_affine<G>, dim3(nblk(count, 256)), dim3(256), 0, s, table_.as<Aff<F>>() + first,
+                     o.as<uint64_t>(), count);
+  MSM_HIP_CHECK(hipGetLastError());
+  MSM_HIP_CHECK(hipMemcpyAsync(out, o.p, count * 96 * G, hipMemcpyDeviceToHost, s));
+  MSM_HIP_CHECK(hipStreamSynchronize(s));
+}
+
+template <int G>
+void Ches<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, hfp::Jac<HF> *out) {
+  typedef typename FieldOf<G>::F F;
+  DeviceGuard g(dev_);
+  if (stride < 32) throw std::runtime_error("CHES scalars must be 32-byte strings");
+  if (n_ == 0) {
+    std::memset(out, 0, sizeof(*out));
+    return;
+  }
+  const size_t n = n_, h = (size_t)p_.h, ne = n * h, NB = B_.size();
+  keys_.ensure(ne * 4);
+  ranks_.ensure(ne * 4);
+  sorted_.ensure(ne * 4);
+  counts_.ensure(NB * 4);
+  offsets_.ensure(NB * 4);
+  order_.ensure(NB * 4);
+  iota_.ensure(NB * 4);
+  sortkeys_.ensure(NB * 4);
+  buckets_.ensure(NB * sizeof(Xyzz<F>));
+  size_t scan_tmp = 0, sort_tmp = 0;
+  hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, counts_.as<uint32_t>(), offsets_.as<uint32_t>(), (int)NB, s);
+  hipcub::DeviceRadixSort::SortPairsDescending(nullptr, sort_tmp, counts_.as<uint32_t>(), sortkeys_.as<uint32_t>(),
+                                               iota_.as<uint32_t>(), order_.as<uint32_t>(), (int)NB, 0, 32, s);
+  tmp_.ensure(std::max(scan_tmp, sort_tmp));
+
+  if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[0], s));
+  MSM_HIP_CHECK(hipMemsetAsync(counts_.p, 0, NB * 4, s));
+  hipLaunchKernelGGL(k_ches_digits, dim3(nblk(n, 256)), dim3(256), 0, s, d_scalars, stride, n, p_.q_exp, p_.h,
+                     hash_.as<uint32_t>(), keys_.as<uint32_t>(), ranks_.as<uint32_t>(), counts_.as<uint32_t>());
+  MSM_HIP_CHECK(hipGetLastError());
+  if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[1], s));
+  size_t tb = tmp_.bytes;
+  MSM_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp_.p, tb, counts_.as<uint32_t>(), offsets_.as<uint32_t>(), (int)NB, s));
+  hipLaunchKernelGGL(k_ches_scatter, dim3(nblk(ne, 256)), dim3(256), 0, s, keys_.as<uint32_t>(), ranks_.as<uint32_t>(),
+                     offsets_.as<uint32_t>(), sorted_.as<uint32_t>(), ne);
+  hipLaunchKernelGGL(k_iota, dim3(nblk(NB, 256)), dim3(256), 0, s, iota_.as<uint32_t>(), NB);
+  tb = tmp_.bytes;
+  MSM_HIP_CHECK(hipcub::DeviceRadixSort::SortPairsDescending(tmp_.p, tb, counts_.as<uint32_t>(), sortkeys_.as<uint32_t>(),
+                                                             iota_.as<uint32_t>(), order_.as<uint32_t>(), (int)NB, 0, 32,
+                                                             s));
+  if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[2], s));
+  hipLaunchKernelGGL(k_accumulate<G>, dim3(nblk(NB, 256)), dim3(256), 0, s, order_.as<uint32_t>(),
+                     counts_.as<uint32_t>(), offsets_.as<uint32_t>(), sorted_.as<uint32_t>(), table_.as<Aff<F>>(),
+                     buckets_.as<Xyzz<F>>(), NB);
+  MSM_HIP_CHECK(hipGetLastError());
+  if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[3], s));
+  red_.launch(s, buckets_.p);
+  if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[4], s));
+  *out = red_.read(s);
+  if (profile_) {
+    MSM_HIP_CHECK(hipEventRecord(ev_[5], s));
+    MSM_HIP_CHECK(hipEventSynchronize(ev_[5]));
+    float ms;
+    MSM_HIP_CHECK(hipEventElapsedTime(&ms, ev_[0], ev_[1]));
+    times_.digits = ms;
+    MSM_HIP_CHECK(hipEventElapsedTime(&ms, ev_[1], ev_[2]));
+    times_.sort = ms;
+    MSM_HIP_CHECK(hipEventElapsedTime(&ms, ev_[2], ev_[3]));
+    times_.accumulate = ms;
+    MSM_HIP_CHECK(hipEventElapsedTime(&ms, ev_[3], ev_[4]));
+    times_.reduce = ms;
+    MSM_HIP_CHECK(hipEventElapsedTime(&ms, ev_[4], ev_[5]));
+    times_.finalize = ms;
+    MSM_HIP_CHECK(hipEventElapsedTime(&ms, ev_[0], ev_[5]));
+    times_.total = ms;
+    times_.accumulate_launches = 1;
+  }
+}
+
+template class Ches<MSM_GROUP>;
+
+}  // namespace msm

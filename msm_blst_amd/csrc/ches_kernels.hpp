@@ -1,0 +1,277 @@
+// ches_kernels.hpp -- device kernels of the CHES "nh + q/5" bucket-set MSM
+// (LuoGuiwen/MSM_blst) for gfx950, templated on the group (G1: Fp, G2: Fp2).
+//
+//   k_ches_table    T[3(i h + j) + m - 1] = m q^j P_i, affine, built on the GPU
+//                   (replaces the 470 s CPU loop of ref main_p1.cpp:155-172):
+//                   xyzz doublings per lane + one Montgomery batch inversion
+//                   per lane over its 3h points
+//   k_ches_digits   MB radix-q digits of every scalar, on device
+//                   (ref auxiliaryfunc.h:92-118 + main_p1.cpp:208-228): std
+//                   q-ary digit + carry -> digit-hash lookup -> (bucket index,
+//                   m, alpha); entries with bucket value 0 are dropped (the
+//                   reference's `if (booth_idx)` guard, multi_scalar.c:440)
+//   k_ches_scatter  counting-sort placement of the (i, j) entries by bucket;
+//                   payload = table slot | sign << 31
+//   k_segsum        segment sums of xyzz points over an index list (the two
+//                   regroupings of the bucket reduction, see ches.hip)
+// Bucket accumulation and the dense window reduction reuse k_accumulate /
+// k_reduce of kernels.hpp.
+#pragma once
+#include "kernels.hpp"
+
+namespace msm {
+
+// packed digit-hash entry (device): bits 0..23 bucket index in B (0 = value 0,
+// skipped), bits 24..25 m - 1, bit 31 alpha (negative digit, carry +1)
+constexpr uint32_t CH_IDX_MASK = 0x00ffffffu;
+
+// ---------------------------------------------------------------- inversion --
+// a^(p-2) mod p (Fermat), fixed 4-bit windows, input any lazy value, output S.
+__device__ constexpr uint64_t PM2[6] = {0xb9feffffffffaaa9ull, 0x1eabfffeb153ffffull, 0x6730d2a0f6b0f624ull,
+                                        0x64774b84f38512bfull, 0x4b1ba7b6434bacd7ull, 0x1a0111ea397fe69aull};
+static __device__ __noinline__ void fp_inv(Fp &r, const Fp &a) {
+  Fp tab[16];
+  fp_one(tab[0]);
+  tab[1] = a;
+  fp_norm(tab[1]);
+  for (int k = 2; k < 16; ++k) fp_mul(tab[k], tab[k - 1], tab[1]);
+  Fp acc;
+  fp_one(acc);
+  for (int nib = 95; nib >= 0; --nib) {
+    if (nib != 95) {
+      for (int k = 0; k < 4; ++k) fp_sqr(acc, acc);
+    }
+    uint32_t w = (uint32_t)(PM2[nib >> 4] >> ((nib & 15) * 4)) & 15u;
+    Fp t = tab[0];
+    for (int k = 1; k < 16; ++k)
+      if ((uint32_t)k == w) t = tab[k];  // uniform per exponent nibble
+    fp_mul(acc, acc, t);
+  }
+  r = acc;
+}
+__device__ __forceinline__ void f_inv(Fp &r, const Fp &a) { fp_inv(r, a); }
+// 1/(a0 + a1 i) = (a0 - a1 i) / (a0^2 + a1^2)
+__device__ __forceinline__ void f_inv(Fp2 &r, const Fp2 &a) {
+  Fp t0, t1, d;
+  fp_sqr(t0, a.c0);
+  fp_sqr(t1, a.c1);
+  fp_add(d, t0, t1);
+  fp_inv(d, d);
+  fp_mul(r.c0, a.c0, d);
+  Fp n1;
+  Fp a1 = a.c1;
+  fp_norm(a1);
+  fp_neg<4>(n1, a1);
+  fp_mul(r.c1, n1, d);
+}
+__device__ __forceinline__ void f_csub(Fp &a) { fp_csub_p(a); }
+__device__ __forceinline__ void f_csub(Fp2 &a) {
+  fp_csub_p(a.c0);
+  fp_csub_p(a.c1);
+}
+
+// ------------------------------------------------------------ table build --
+// One lane per base point i in [i0, i0+cnt).  scratch holds the lane's 3h
+// xyzz points and prefix products, interleaved by lane for coalescing.
+template <int G>
+static __global__ void __launch_bounds__(256)
+    k_ches_table(const Aff<typename FieldOf<G>::F> *__restrict__ P, size_t i0, size_t cnt, int q_exp, int h,
+                 Xyzz<typename FieldOf<G>::F> *__restrict__ scratch, typename FieldOf<G>::F *__restrict__ pref,
+                 Aff<typename FieldOf<G>::F> *__restrict__ T) {
+  typedef typename FieldOf<G>::F F;
+  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= cnt) return;
+  const size_t i = i0 + t;
+  const int K = 3 * h;
+  Aff<F> p = ld16(&P[i]);
+  Aff<F> *out = T + (size_t)K * i;
+  if (f_is_zero_exact(p.x) && f_is_zero_exact(p.y)) {  // infinity: every multiple is infinity
+    Aff<F> z;
+    f_zero(z.x);
+    f_zero(z.y);
+    for (int k = 0; k < K; ++k) st16(&out[k], z);
+    return;
+  }
+  Xyzz<F> Q;
+  xyzz_from_aff(Q, p, false);
+  for (int j = 0; j < h; ++j) {
+    Xyzz<F> Q2, Q3;
+    xyzz_dbl(Q2, Q);
+    Q3 = Q2;
+    xyzz_add(Q3, Q);
+    st16(&scratch[(size_t)(3 * j) * cnt + t], Q);
+    st16(&scratch[(size_t)(3 * j + 1) * cnt + t], Q2);
+    st16(&scratch[(size_t)(3 * j + 2) * cnt + t], Q3);
+    if (j + 1 < h)
+      for (int e = 0; e < q_exp; ++e) {
+        Xyzz<F> tmp = Q;
+        xyzz_dbl(Q, tmp);
+      }
+  }
+  // Montgomery batch inversion of u_k = ZZ_k * ZZZ_k  (1/ZZ = ZZZ/u, 1/ZZZ = ZZ/u)
+  F c;
+  f_one(c);
+  for (int k = 0; k < K; ++k) {
+    Xyzz<F> a = ld16(&scratch[(size_t)k * cnt + t]);
+    F u;
+    f_mul(u, a.zz, a.zzz);
+    f_mul(c, c, u);
+    pref[(size_t)k * cnt + t] = c;
+  }
+  F inv;
+  f_inv(inv, c);
+  for (int k = K - 1; k >= 0; --k) {
+    Xyzz<F> a = ld16(&scratch[(size_t)k * cnt + t]);
+    F ik;
+    if (k > 0) {
+      F pk = pref[(size_t)(k - 1) * cnt + t];
+      f_mul(ik, inv, pk);
+      F u;
+      f_mul(u, a.zz, a.zzz);
+      f_mul(inv, inv, u);
+    } else {
+      ik = inv;
+    }
+    F izz, izzz;
+    f_mul(izz, ik, a.zzz);
+    f_mul(izzz, ik, a.zz);
+    Aff<F> r;
+    f_mul(r.x, a.x, izz);
+    f_mul(r.y, a.y, izzz);
+    f_csub(r.x);
+    f_csub(r.y);
+    st16(&out[k], r);
+  }
+}
+
+// internal affine -> blst affine (canonical Montgomery, R = 2^384)
+template <int G>
+__global__ void k_export_affine(const Aff<typename FieldOf<G>::F> *__restrict__ in, uint64_t *__restrict__ out,
+                                size_t n) {
+  typedef typename FieldOf<G>::F F;
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Aff<F> a = ld16(&in[i]);
+  uint64_t *o = out + i * 12 * G;
+  if (f_is_zero_exact(a.x) && f_is_zero_exact(a.y)) {
+    for (int k = 0; k < 12 * G; ++k) o[k] = 0;
+    return;
+  }
+  f_to_blst(o, a.x);
+  f_to_blst(o + 6 * G, a.y);
+}
+
+// ------------------------------------------------------------------ digits --
+// r (BLS12-381 group order), little-endian 32-bit words
+__device__ constexpr uint32_t FR_R32[8] = {0x00000001u, 0xffffffffu, 0xfffe5bfeu, 0x53bda402u,
+                                           0x09a1d805u, 0x3339d808u, 0x299d7d48u, 0x73eda753u};
+
+// s >= r ? s - r : s   (on 8 x 32-bit words)
+__device__ __forceinline__ void sub_r_if_ge(uint32_t s[8]) {
+  uint32_t t[8];
+  int64_t br = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    int64_t d = (int64_t)s[k] - (int64_t)FR_R32[k] + br;
+    t[k] = (uint32_t)d;
+    br = d >> 32;
+  }
+  bool ge = br == 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s[k] = ge ? t[k] : s[k];
+}
+
+// One lane per scalar.  Scalars >= r are reduced mod r first (the reference
+// requires s < r for this method, SURVEY 8b "Errors"; reducing keeps the result
+// equal to sum s_i P_i for points of order r).
+static __global__ void __launch_bounds__(256)
+    k_ches_digits(const uint8_t *__restrict__ scalars, size_t stride, size_t n, int q_exp, int h,
+                  const uint32_t *__restrict__ hash, uint32_t *__restrict__ keys, uint32_t *__restrict__ ranks,
+                  uint32_t *__restrict__ counts) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t *sp = scalars + i * stride;
+  uint32_t s[10];
+  if ((stride & 3) == 0) {
+    const uint32_t *s32 = reinterpret_cast<const uint32_t *>(sp);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s[k] = s32[k];
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      s[k] = (uint32_t)sp[4 * k] | ((uint32_t)sp[4 * k + 1] << 8) | ((uint32_t)sp[4 * k + 2] << 16) |
+             ((uint32_t)sp[4 * k + 3] << 24);
+  }
+  sub_r_if_ge(s);
+  sub_r_if_ge(s);
+  s[8] = s[9] = 0;
+  const uint32_t qmask = (1u << q_exp) - 1u;
+  uint32_t carry = 0;
+  for (int j = 0; j < h; ++j) {
+    int off = j * q_exp;
+    int wi = off >> 5, sh = off & 31;
+    uint32_t lo = wi < 10 ? s[wi] : 0u, hi = wi + 1 < 10 ? s[wi + 1] : 0u;
+    uint32_t d = (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) & qmask;
+    uint32_t e = hash[d + carry];
+    carry = e >> 31;
+    size_t k = i * (size_t)h + j;
+    uint32_t b = e & CH_IDX_MASK;
+    if (b) {
+      ranks[k] = atomicAdd(&counts[b], 1u);
+      keys[k] = e;
+    } else {
+      keys[k] = KEY_NONE;
+    }
+  }
+}
+
+static __global__ void k_ches_scatter(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ ranks,
+                               const uint32_t *__restrict__ offsets, uint32_t *__restrict__ sorted, size_t ne) {
+  size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= ne) return;
+  uint32_t k = keys[e];
+  if (k == KEY_NONE) return;
+  uint32_t b = k & CH_IDX_MASK, m1 = (k >> 24) & 3u;
+  sorted[offsets[b] + ranks[e]] = (uint32_t)(3 * e + m1) | (k & 0x80000000u);
+}
+
+// ------------------------------------------------------------ segment sums --
+// dst[t] = sum_{k in [starts[t], starts[t+1])} src[idx ? idx[k] : k]   (xyzz)
+template <int G>
+static __global__ void __launch_bounds__(256)
+    k_segsum(const Xyzz<typename FieldOf<G>::F> *__restrict__ src, const uint32_t *__restrict__ idx,
+             const uint32_t *__restrict__ starts, Xyzz<typename FieldOf<G>::F> *__restrict__ dst, size_t nout) {
+  typedef typename FieldOf<G>::F F;
+  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nout) return;
+  uint32_t lo = starts[t], hi = starts[t + 1];
+  Xyzz<F> acc;
+  if (lo == hi) {
+    xyzz_set_inf(acc);
+  } else {
+    acc = ld16(&src[idx ? idx[lo] : lo]);
+    for (uint32_t k = lo + 1; k < hi; ++k) {
+      Xyzz<F> a = ld16(&src[idx ? idx[k] : k]);
+      xyzz_add(acc, a);
+    }
+  }
+  st16(&dst[t], acc);
+}
+
+// blst xyzz {x, y, zzz, zz} (Montgomery R=2^384) -> internal xyzz
+template <int G>
+__global__ void k_import_xyzz(const uint64_t *__restrict__ in, Xyzz<typename FieldOf<G>::F> *__restrict__ out,
+                              size_t n) {
+  typedef typename FieldOf<G>::F F;
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t *p = in + i * 24 * G;
+  Xyzz<F> a;
+  f_from_blst(a.x, p);
+  f_from_blst(a.y, p + 6 * G);
+  f_from_blst(a.zzz, p + 12 * G);
+  f_from_blst(a.zz, p + 18 * G);
+  st16(&out[i], a);
+}
+
+}  // namespace msm

@@ -6,9 +6,14 @@
 #include "engine.hpp"
 #include "kernels.hpp"
 
+// compiled once per group (build.py: -DMSM_GROUP=1 and -DMSM_GROUP=2) so the
+// two instantiations build in parallel
+#ifndef MSM_GROUP
+#error "define MSM_GROUP (1 or 2)"
+#endif
+
 namespace msm {
 
-static inline unsigned nblk(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
 
 template <int G>
 Pippenger<G>::Pippenger(int device, int window_bits) : dev_(device), c_(window_bits) {
@@ -97,11 +102,6 @@ void Pippenger<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, i
   iota_.ensure(NT * 4);
   sortkeys_.ensure(NT * 4);
   buckets_.ensure(NT * sizeof(Xyzz<F>));
-  redA_[0].ensure(NT / 2 * sizeof(Xyzz<F>) + 64);
-  redA_[1].ensure(NT / 2 * sizeof(Xyzz<F>) + 64);
-  redY_[0].ensure(NT / 2 * sizeof(Xyzz<F>) + 64);
-  redY_[1].ensure(NT / 2 * sizeof(Xyzz<F>) + 64);
-  fin_.ensure((size_t)W * 144 * G);
 
   size_t scan_tmp = 0, sort_tmp = 0;
   hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, counts_.as<uint32_t>(), offsets_.as<uint32_t>(), (int)NT, s);
@@ -130,37 +130,13 @@ void Pippenger<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, i
                      buckets_.as<Xyzz<F>>(), NT);
   MSM_HIP_CHECK(hipGetLastError());
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[3], s));
-  // bucket reduction levels
-  const Xyzz<F> *A = buckets_.as<Xyzz<F>>();
-  const Xyzz<F> *Y = nullptr;
-  int S = (int)NB, lvl = 0;
-  while (S > 1) {
-    int L = S >= 8 ? 8 : S;
-    int log2L = L == 8 ? 3 : (L == 4 ? 2 : 1);
-    Xyzz<F> *A2 = redA_[lvl & 1].as<Xyzz<F>>();
-    Xyzz<F> *Y2 = redY_[lvl & 1].as<Xyzz<F>>();
-    size_t threads = (size_t)W * (S / L);
-    hipLaunchKernelGGL(k_reduce<G>, dim3(nblk(threads, 64)), dim3(64), 0, s, A, Y, A2, Y2, S, L, log2L, W);
-    MSM_HIP_CHECK(hipGetLastError());
-    A = A2;
-    Y = Y2;
-    S /= L;
-    ++lvl;
-  }
+  std::vector<hfp::Jac<HF>> T;
+  dense_.launch(s, buckets_.p, W, (int)NB);
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[4], s));
-  hipLaunchKernelGGL(k_finalize<G>, dim3(1), dim3(64), 0, s, Y, fin_.as<uint64_t>(), W);
-  MSM_HIP_CHECK(hipGetLastError());
-  std::vector<hfp::Jac<HF>> T(W);
-  MSM_HIP_CHECK(hipMemcpyAsync(T.data(), fin_.p, (size_t)W * sizeof(hfp::Jac<HF>), hipMemcpyDeviceToHost, s));
+  dense_.read(s, W, T);
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[5], s));
   MSM_HIP_CHECK(hipStreamSynchronize(s));
-  // Horner over windows: ret = sum_w 2^(c w) T_w (ref multi_scalar.c:565-575)
-  ret = T[W - 1];
-  for (int w = W - 2; w >= 0; --w) {
-    for (int k = 0; k < c; ++k) ret = hfp::dbl(ret);
-    ret = hfp::addj(ret, T[w]);
-  }
-  *out = ret;
+  *out = horner(T, c);
   if (profile_) {
     float ms;
     MSM_HIP_CHECK(hipEventElapsedTime(&ms, ev_[0], ev_[1]));
@@ -179,8 +155,43 @@ void Pippenger<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, i
   }
 }
 
-template class Pippenger<1>;
-template class Pippenger<2>;
+template <int G>
+void DenseReducer<G>::launch(hipStream_t s, const void *Abuf, int W, int S) {
+  typedef typename FieldOf<G>::F F;
+  const size_t NT = (size_t)W * S;
+  for (int k = 0; k < 2; ++k) {
+    redA[k].ensure(NT / 2 * sizeof(Xyzz<F>) + 64);
+    redY[k].ensure(NT / 2 * sizeof(Xyzz<F>) + 64);
+  }
+  fin.ensure((size_t)W * 144 * G);
+  const Xyzz<F> *A = reinterpret_cast<const Xyzz<F> *>(Abuf);
+  const Xyzz<F> *Y = nullptr;
+  int Sc = S, lvl = 0;
+  while (Sc > 1) {
+    int L = Sc >= 8 ? 8 : Sc;
+    int log2L = L == 8 ? 3 : (L == 4 ? 2 : 1);
+    Xyzz<F> *A2 = redA[lvl & 1].as<Xyzz<F>>();
+    Xyzz<F> *Y2 = redY[lvl & 1].as<Xyzz<F>>();
+    size_t threads = (size_t)W * (Sc / L);
+    hipLaunchKernelGGL(k_reduce<G>, dim3(nblk(threads, 64)), dim3(64), 0, s, A, Y, A2, Y2, Sc, L, log2L, W);
+    MSM_HIP_CHECK(hipGetLastError());
+    A = A2;
+    Y = Y2;
+    Sc /= L;
+    ++lvl;
+  }
+  if (Y == nullptr) Y = A;  // S == 1
+  hipLaunchKernelGGL(k_finalize<G>, dim3(nblk(W, 64)), dim3(64), 0, s, Y, fin.as<uint64_t>(), W);
+  MSM_HIP_CHECK(hipGetLastError());
+}
+template <int G>
+void DenseReducer<G>::read(hipStream_t s, int W, std::vector<hfp::Jac<HF>> &out) {
+  out.resize(W);
+  MSM_HIP_CHECK(hipMemcpyAsync(out.data(), fin.p, (size_t)W * sizeof(hfp::Jac<HF>), hipMemcpyDeviceToHost, s));
+  MSM_HIP_CHECK(hipStreamSynchronize(s));
+}
+template struct DenseReducer<MSM_GROUP>;
+template class Pippenger<MSM_GROUP>;
 
 // ---------------------------------------------------------------------------
 // device unit-test entry points (parity tests of the field / curve layers)
@@ -269,9 +280,7 @@ void test_xyzz(const uint64_t *pts, size_t npts, const uint32_t *ops, int len, s
   MSM_HIP_CHECK(hipGetLastError());
   MSM_HIP_CHECK(hipMemcpy(out, dout.p, nseq * 2 * 144 * G, hipMemcpyDeviceToHost));
 }
-template void test_field<1>(int, const uint64_t *, const uint64_t *, uint64_t *, size_t);
-template void test_field<2>(int, const uint64_t *, const uint64_t *, uint64_t *, size_t);
-template void test_xyzz<1>(const uint64_t *, size_t, const uint32_t *, int, size_t, uint64_t *);
-template void test_xyzz<2>(const uint64_t *, size_t, const uint32_t *, int, size_t, uint64_t *);
+template void test_field<MSM_GROUP>(int, const uint64_t *, const uint64_t *, uint64_t *, size_t);
+template void test_xyzz<MSM_GROUP>(const uint64_t *, size_t, const uint32_t *, int, size_t, uint64_t *);
 
 }  // namespace msm

@@ -19,12 +19,15 @@
 
 namespace msm {
 
+inline unsigned nblk(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
+
 struct DevBuf {
   void *p = nullptr;
   size_t bytes = 0;
   DevBuf() = default;
   DevBuf(const DevBuf &) = delete;
   DevBuf &operator=(const DevBuf &) = delete;
+  DevBuf(DevBuf &&o) noexcept : p(o.p), bytes(o.bytes) { o.p = nullptr, o.bytes = 0; }
   ~DevBuf() { release(); }
   void release() {
     if (p) (void)hipFree(p);
@@ -60,6 +63,29 @@ struct HostField<2> {
   typedef hfp::Fp2 F;
 };
 
+// Dense windowed bucket reduction: for each of W windows of S buckets
+// (A[w*S + b-1] holds bucket value b), T_w = sum_b b * A_b, read back to host
+// as blst Jacobians.  Shared by the Pippenger and CHES pipelines.
+template <int G>
+struct DenseReducer {
+  typedef typename HostField<G>::F HF;
+  DevBuf redA[2], redY[2], fin;
+  // A: device array of W*S internal xyzz points; enqueues the reduction levels
+  void launch(hipStream_t s, const void *A, int W, int S);
+  // enqueue the read-back of the W window totals and wait for it
+  void read(hipStream_t s, int W, std::vector<hfp::Jac<HF>> &out);
+};
+// sum_w 2^(c w) T_w, Horner from the top window (ref multi_scalar.c:565-575)
+template <class HF>
+hfp::Jac<HF> horner(const std::vector<hfp::Jac<HF>> &T, int c) {
+  hfp::Jac<HF> ret = T.back();
+  for (int w = (int)T.size() - 2; w >= 0; --w) {
+    for (int k = 0; k < c; ++k) ret = hfp::dbl(ret);
+    ret = hfp::addj(ret, T[w]);
+  }
+  return ret;
+}
+
 // Plain Pippenger bucket method (ref src/multi_scalar.c:549-576) on one GPU.
 template <int G>
 class Pippenger {
@@ -82,8 +108,76 @@ class Pippenger {
   size_t n_ = 0;
   bool profile_ = false;
   PhaseTimes times_;
-  DevBuf pts_, keys_, ranks_, counts_, offsets_, sorted_, order_, iota_, sortkeys_, buckets_, redA_[2], redY_[2],
-      fin_, tmp_;
+  DevBuf pts_, keys_, ranks_, counts_, offsets_, sorted_, order_, iota_, sortkeys_, buckets_, tmp_;
+  DenseReducer<G> dense_;
+  std::vector<hipEvent_t> ev_;
+};
+
+// ---------------------------------------------------------------------------
+// CHES "nh + q/5" bucket-set method (ches.hip)
+// ---------------------------------------------------------------------------
+// parameters of ref ches_config_files/config_file_n_exp_*.h
+struct ChesParams {
+  int n_exp, beta, q_exp, h, a_h, d_max, b_size, q_exp_bgmw, h_bgmw;
+};
+bool ches_params_for(int n_exp, int beta, ChesParams *out);
+// bucket set B of ref auxiliaryfunc.h:257-288 (ascending)
+std::vector<int> ches_bucket_set(int q, int a_h);
+// packed digit hash (ches_kernels.hpp layout) of ref main_p1.cpp:140-152, q+1 entries
+std::vector<uint32_t> ches_digit_hash(const std::vector<int> &B, int q);
+
+// sum_{i >= 1} B[i] * S_i for ascending weights B (B[0] = 0) over device xyzz
+// buckets S (replaces ref multi_scalar.c:301-321).  Two regroupings by the low
+// and high halves of B[i] (2 xyzz adds per bucket) and one dense 2-window
+// reduction; the plan depends only on B and is built once.
+template <int G>
+class WeightedReducer {
+ public:
+  typedef typename HostField<G>::F HF;
+  void plan(const std::vector<int> &B);
+  void launch(hipStream_t s, const void *S);   // device xyzz[|B|]
+  hfp::Jac<HF> read(hipStream_t s);             // waits
+  size_t size() const { return bsize_; }
+
+ private:
+  size_t bsize_ = 0, final_perm_off_ = 0;
+  int sbits_ = 1;
+  DevBuf idx_, dense_buf_, part_[2];
+  std::vector<DevBuf> starts_;
+  std::vector<size_t> nout_;
+  DenseReducer<G> dense_;
+};
+
+template <int G>
+class Ches {
+ public:
+  typedef typename HostField<G>::F HF;
+  Ches(int device, const ChesParams &p);
+  ~Ches();
+  // base points (blst affine, host or device) -> table T of 3 n h points, built on the GPU
+  void build_table(const void *points_blst, size_t n, bool on_device, hipStream_t s);
+  // a precomputed table T (blst affine layout, 3 n h points), host or device
+  void set_table(const void *table_blst, size_t n, bool on_device, hipStream_t s);
+  // copy T[first, first+count) back in blst affine layout (host memory)
+  void get_table(void *out_blst, size_t first, size_t count, hipStream_t s);
+  // scalars: n 32-byte LE strings (stride >= 32) on device
+  void run(hipStream_t s, const uint8_t *d_scalars, size_t stride, hfp::Jac<HF> *out);
+  size_t npoints() const { return n_; }
+  const ChesParams &params() const { return p_; }
+  size_t bucket_count() const { return B_.size(); }
+  void set_profiling(bool on) { profile_ = on; }
+  const PhaseTimes &times() const { return times_; }
+  int device() const { return dev_; }
+
+ private:
+  int dev_;
+  ChesParams p_;
+  std::vector<int> B_;
+  size_t n_ = 0;
+  bool profile_ = false;
+  PhaseTimes times_;
+  DevBuf hash_, table_, keys_, ranks_, counts_, offsets_, sorted_, order_, iota_, sortkeys_, buckets_, tmp_;
+  WeightedReducer<G> red_;
   std::vector<hipEvent_t> ev_;
 };
 

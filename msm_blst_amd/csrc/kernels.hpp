@@ -206,7 +206,7 @@ __global__ void k_scatter(const uint32_t *__restrict__ keys, const uint32_t *__r
   sorted[pos] = (uint32_t)i | (k & 0x80000000u);
 }
 
-__global__ void k_iota(uint32_t *a, size_t n) {
+static __global__ void k_iota(uint32_t *a, size_t n) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) a[i] = (uint32_t)i;
 }
