@@ -101,37 +101,70 @@ std::vector<uint32_t> ches_digit_hash(const std::vector<int> &B, int q) {
 }
 #endif  // MSM_GROUP == 1
 
-// ---------------------------------------------------------- reduction plan --
-// sum_i B[i] S_i = sum_u u L_u + 2^s sum_v v H_v  with u = B[i] mod 2^s,
-// v = B[i] >> s, L_u = sum_{i: low(B[i]) = u} S_i, H_v = sum_{i: high(B[i]) = v} S_i.
-// L and H are segment sums over one list of 2(|B|-1) bucket indices (level 0:
-// chunks of <= 8 within a segment; then pairwise levels until one partial per
-// segment; then a dense scatter into 2 windows of 2^s slots), followed by the
-// dense 2-window reduction and a 2^s Horner step on the host.
+// -------------------------------------------------------------- scan reduce --
 template <int G>
-void WeightedReducer<G>::plan(const std::vector<int> &B) {
+void ScanReducer<G>::launch(hipStream_t s, const void *Abuf, int W, int S) {
   typedef typename FieldOf<G>::F F;
-  bsize_ = B.size();
+  if (S < 1 || (S & (S - 1))) throw std::runtime_error("ScanReducer: S must be a power of two");
+  const size_t NT = (size_t)W * S;
+  buf[0].ensure(NT * sizeof(Xyzz<F>));
+  buf[1].ensure(NT * sizeof(Xyzz<F>));
+  fin.ensure((size_t)W * 144 * G);
+  const Xyzz<F> *src = reinterpret_cast<const Xyzz<F> *>(Abuf);
+  int cur = 0;
+  for (int d = 1; d < S; d <<= 1) {  // suffix sums T_k = sum_{b >= k} A_b
+    Xyzz<F> *dst = buf[cur].as<Xyzz<F>>();
+    hipLaunchKernelGGL(k_suffix_step<G>, dim3(nblk(NT, 64)), dim3(64), 0, s, src, dst, S, d, W);
+    MSM_HIP_CHECK(hipGetLastError());
+    src = dst;
+    cur ^= 1;
+  }
+  for (size_t len = NT; len > (size_t)W; len >>= 1) {  // sum_k T_k = sum_b b A_b
+    Xyzz<F> *dst = buf[cur].as<Xyzz<F>>();
+    hipLaunchKernelGGL(k_pair_step<G>, dim3(nblk(len / 2, 64)), dim3(64), 0, s, src, dst, len / 2);
+    MSM_HIP_CHECK(hipGetLastError());
+    src = dst;
+    cur ^= 1;
+  }
+  hipLaunchKernelGGL(k_finalize<G>, dim3(nblk(W, 64)), dim3(64), 0, s, src, fin.as<uint64_t>(), W);
+  MSM_HIP_CHECK(hipGetLastError());
+}
+template <int G>
+void ScanReducer<G>::read(hipStream_t s, int W, std::vector<hfp::Jac<HF>> &out) {
+  out.resize(W);
+  MSM_HIP_CHECK(hipMemcpyAsync(out.data(), fin.p, (size_t)W * sizeof(hfp::Jac<HF>), hipMemcpyDeviceToHost, s));
+  MSM_HIP_CHECK(hipStreamSynchronize(s));
+}
+template struct ScanReducer<MSM_GROUP>;
+
+// ---------------------------------------------------------- reduction plan --
+// sum_i w_i S_i = sum_u u L_u + 2^s sum_v v H_v  with u = w_i mod 2^s,
+// v = w_i >> s, L_u = sum_{i: low(w_i) = u} S_i, H_v = sum_{i: high(w_i) = v} S_i.
+// L and H are segment sums over one list of bucket indices (level 0: chunks of
+// <= 8 within a segment; then pairwise levels until one partial per segment;
+// then a dense scatter into 2 windows of 2^s slots), followed by the dense
+// 2-window ScanReducer and a 2^s Horner step on the host.
+template <int G>
+void WeightedReducer<G>::plan(const std::vector<uint32_t> &w) {
+  typedef typename FieldOf<G>::F F;
+  bsize_ = w.size();
   starts_.clear();
   nout_.clear();
-  int maxB = B.empty() ? 0 : B.back();
-  for (size_t i = 1; i < B.size(); ++i)
-    if (B[i] <= B[i - 1]) throw std::runtime_error("bucket set must be strictly ascending");
-  if (!B.empty() && B[0] != 0) throw std::runtime_error("bucket set must start with 0");
+  uint32_t maxw = 0;
+  for (uint32_t x : w) maxw = std::max(maxw, x);
   int bits = 0;
-  while (bits < 31 && (1 << bits) <= maxB) ++bits;
+  while (bits < 32 && ((uint64_t)1 << bits) <= maxw) ++bits;
   sbits_ = std::max(1, (bits + 1) / 2);
   const uint32_t S = 1u << sbits_;
-  std::vector<uint32_t> idx, seg;
-  for (size_t i = 1; i < B.size(); ++i) {  // high halves, ascending v
-    uint32_t v = (uint32_t)B[i] >> sbits_;
-    if (v) idx.push_back((uint32_t)i), seg.push_back(S + v - 1);
-  }
-  std::vector<std::vector<uint32_t>> byu(S);
-  for (size_t i = 1; i < B.size(); ++i) {
-    uint32_t u = (uint32_t)B[i] & (S - 1);
+  std::vector<std::vector<uint32_t>> byv(S), byu(S);
+  for (size_t i = 0; i < w.size(); ++i) {
+    uint32_t v = w[i] >> sbits_, u = w[i] & (S - 1);
+    if (v) byv[v].push_back((uint32_t)i);
     if (u) byu[u].push_back((uint32_t)i);
   }
+  std::vector<uint32_t> idx, seg;
+  for (uint32_t v = 1; v < S; ++v)
+    for (uint32_t i : byv[v]) idx.push_back(i), seg.push_back(S + v - 1);
   for (uint32_t u = 1; u < S; ++u)
     for (uint32_t i : byu[u]) idx.push_back(i), seg.push_back(u - 1);
   // level 0 + pairwise levels
@@ -158,30 +191,24 @@ void WeightedReducer<G>::plan(const std::vector<int> &B) {
     C = 2;
     if (cur_seg.empty()) break;
   }
-  // dense scatter: slot -> its single partial (or empty)
-  std::vector<uint32_t> dst(2 * S + 1, 0);
-  {
-    std::vector<int> at(2 * S, -1);
-    for (size_t k = 0; k < cur_seg.size(); ++k) at[cur_seg[k]] = (int)k;
-    // express as CSR over the partial array: ranges of length 0/1 need a permuted
-    // index, so the final level uses idx = perm with starts 0..count
-    std::vector<uint32_t> perm;
-    for (uint32_t sl = 0; sl < 2 * S; ++sl) {
-      dst[sl] = (uint32_t)perm.size();
-      if (at[sl] >= 0) perm.push_back((uint32_t)at[sl]);
-    }
-    dst[2 * S] = (uint32_t)perm.size();
-    starts_.emplace_back();
-    starts_.back().ensure(dst.size() * 4);
-    MSM_HIP_CHECK(hipMemcpy(starts_.back().p, dst.data(), dst.size() * 4, hipMemcpyHostToDevice));
-    nout_.push_back(2 * S);
-    // idx buffer: [level-0 item list | final permutation]
-    std::vector<uint32_t> all = idx;
-    all.insert(all.end(), perm.begin(), perm.end());
-    idx_.ensure(std::max<size_t>(all.size(), 1) * 4);
-    if (!all.empty()) MSM_HIP_CHECK(hipMemcpy(idx_.p, all.data(), all.size() * 4, hipMemcpyHostToDevice));
-    final_perm_off_ = idx.size();
+  // dense scatter: slot -> its single partial (or empty), via a permutation
+  std::vector<uint32_t> dst(2 * S + 1, 0), perm;
+  std::vector<int> at(2 * S, -1);
+  for (size_t k = 0; k < cur_seg.size(); ++k) at[cur_seg[k]] = (int)k;
+  for (uint32_t sl = 0; sl < 2 * S; ++sl) {
+    dst[sl] = (uint32_t)perm.size();
+    if (at[sl] >= 0) perm.push_back((uint32_t)at[sl]);
   }
+  dst[2 * S] = (uint32_t)perm.size();
+  starts_.emplace_back();
+  starts_.back().ensure(dst.size() * 4);
+  MSM_HIP_CHECK(hipMemcpy(starts_.back().p, dst.data(), dst.size() * 4, hipMemcpyHostToDevice));
+  nout_.push_back(2 * S);
+  std::vector<uint32_t> all = idx;  // [level-0 item list | final permutation]
+  all.insert(all.end(), perm.begin(), perm.end());
+  idx_.ensure(std::max<size_t>(all.size(), 1) * 4);
+  if (!all.empty()) MSM_HIP_CHECK(hipMemcpy(idx_.p, all.data(), all.size() * 4, hipMemcpyHostToDevice));
+  final_perm_off_ = idx.size();
   size_t maxp = 1;
   for (size_t l = 0; l + 1 < nout_.size(); ++l) maxp = std::max(maxp, nout_[l]);
   part_[0].ensure(maxp * sizeof(Xyzz<F>));
@@ -199,7 +226,6 @@ void WeightedReducer<G>::launch(hipStream_t s, const void *Sbuf) {
     const bool last = l + 1 == L;
     Xyzz<F> *dst = last ? dense_buf_.as<Xyzz<F>>() : part_[l & 1].as<Xyzz<F>>();
     const uint32_t *ix = l == 0 ? idx : (last ? idx + final_perm_off_ : nullptr);
-    if (last && L == 1) src = reinterpret_cast<const Xyzz<F> *>(Sbuf);  // no items at all
     if (nout_[l])
       hipLaunchKernelGGL(k_segsum<G>, dim3(nblk(nout_[l], 64)), dim3(64), 0, s, src, ix, starts_[l].as<uint32_t>(),
                          dst, nout_[l]);
@@ -232,13 +258,32 @@ Ches<G>::Ches(int device, const ChesParams &p) : dev_(device), p_(p) {
   std::vector<uint32_t> H = ches_digit_hash(B_, q);
   hash_.ensure(H.size() * 4);
   MSM_HIP_CHECK(hipMemcpy(hash_.p, H.data(), H.size() * 4, hipMemcpyHostToDevice));
-  red_.plan(B_);
+  for (size_t k = 1; k < B_.size() && B_[k] <= p.a_h + 1; ++k) small_ = (int)k;
+  plan_buckets(0);
   ev_.resize(8);
   for (auto &e : ev_) MSM_HIP_CHECK(hipEventCreate(&e));
 }
 template <int G>
 Ches<G>::~Ches() {
   for (auto &e : ev_) (void)hipEventDestroy(e);
+}
+
+// bucket space = B plus (copies_ - 1) copies of the small buckets 1..small_;
+// copies_ is chosen so a copy receives ~12 top-digit entries (n / (small_ copies))
+template <int G>
+void Ches<G>::plan_buckets(size_t n) {
+  int want = 1;
+  if (small_ > 0 && n > 0) {
+    size_t c = (n + (size_t)small_ * 12 - 1) / ((size_t)small_ * 12);
+    want = (int)std::min<size_t>(std::max<size_t>(c, 1), 256);
+  }
+  if (want == copies_ && red_.size()) return;
+  copies_ = want;
+  std::vector<uint32_t> w(B_.begin(), B_.end());
+  for (int c = 1; c < copies_; ++c)
+    for (int k = 1; k <= small_; ++k) w.push_back((uint32_t)B_[k]);
+  if (w.size() >= (1u << 24)) throw std::runtime_error("CHES bucket space exceeds 24-bit indices");
+  red_.plan(w);
 }
 
 template <int G>
@@ -276,6 +321,7 @@ void Ches<G>::build_table(const void *pts, size_t n, bool on_device, hipStream_t
   }
   MSM_HIP_CHECK(hipStreamSynchronize(s));
   n_ = n;
+  plan_buckets(n);
 }
 
 template <int G>
@@ -298,6 +344,7 @@ void Ches<G>::set_table(const void *tab, size_t n, bool on_device, hipStream_t s
   MSM_HIP_CHECK(hipGetLastError());
   MSM_HIP_CHECK(hipStreamSynchronize(s));
   n_ = n;
+  plan_buckets(n);
 }
 
 template <int G>
@@ -324,7 +371,7 @@ void Ches<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, hfp::J
     std::memset(out, 0, sizeof(*out));
     return;
   }
-  const size_t n = n_, h = (size_t)p_.h, ne = n * h, NB = B_.size();
+  const size_t n = n_, h = (size_t)p_.h, ne = n * h, NB = bucket_count();
   keys_.ensure(ne * 4);
   ranks_.ensure(ne * 4);
   sorted_.ensure(ne * 4);
@@ -336,14 +383,17 @@ void Ches<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, hfp::J
   buckets_.ensure(NB * sizeof(Xyzz<F>));
   size_t scan_tmp = 0, sort_tmp = 0;
   hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, counts_.as<uint32_t>(), offsets_.as<uint32_t>(), (int)NB, s);
+  int sort_bits = 1;  // counts <= ne
+  while (sort_bits < 32 && ((size_t)1 << sort_bits) <= ne) ++sort_bits;
   hipcub::DeviceRadixSort::SortPairsDescending(nullptr, sort_tmp, counts_.as<uint32_t>(), sortkeys_.as<uint32_t>(),
-                                               iota_.as<uint32_t>(), order_.as<uint32_t>(), (int)NB, 0, 32, s);
+                                               iota_.as<uint32_t>(), order_.as<uint32_t>(), (int)NB, 0, sort_bits, s);
   tmp_.ensure(std::max(scan_tmp, sort_tmp));
 
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[0], s));
   MSM_HIP_CHECK(hipMemsetAsync(counts_.p, 0, NB * 4, s));
   hipLaunchKernelGGL(k_ches_digits, dim3(nblk(n, 256)), dim3(256), 0, s, d_scalars, stride, n, p_.q_exp, p_.h,
-                     hash_.as<uint32_t>(), keys_.as<uint32_t>(), ranks_.as<uint32_t>(), counts_.as<uint32_t>());
+                     hash_.as<uint32_t>(), keys_.as<uint32_t>(), ranks_.as<uint32_t>(), counts_.as<uint32_t>(),
+                     (uint32_t)B_.size(), (uint32_t)small_, (uint32_t)copies_);
   MSM_HIP_CHECK(hipGetLastError());
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[1], s));
   size_t tb = tmp_.bytes;
@@ -353,8 +403,8 @@ void Ches<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, hfp::J
   hipLaunchKernelGGL(k_iota, dim3(nblk(NB, 256)), dim3(256), 0, s, iota_.as<uint32_t>(), NB);
   tb = tmp_.bytes;
   MSM_HIP_CHECK(hipcub::DeviceRadixSort::SortPairsDescending(tmp_.p, tb, counts_.as<uint32_t>(), sortkeys_.as<uint32_t>(),
-                                                             iota_.as<uint32_t>(), order_.as<uint32_t>(), (int)NB, 0, 32,
-                                                             s));
+                                                             iota_.as<uint32_t>(), order_.as<uint32_t>(), (int)NB, 0,
+                                                             sort_bits, s));
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[2], s));
   hipLaunchKernelGGL(k_accumulate<G>, dim3(nblk(NB, 256)), dim3(256), 0, s, order_.as<uint32_t>(),
                      counts_.as<uint32_t>(), offsets_.as<uint32_t>(), sorted_.as<uint32_t>(), table_.as<Aff<F>>(),

@@ -184,10 +184,12 @@ __device__ __forceinline__ void sub_r_if_ge(uint32_t s[8]) {
 // One lane per scalar.  Scalars >= r are reduced mod r first (the reference
 // requires s < r for this method, SURVEY 8b "Errors"; reducing keeps the result
 // equal to sum s_i P_i for points of order r).
+// Top-digit entries whose bucket index k is <= small go to copy i % copies of
+// bucket k (copy 0 = k itself, copy c >= 1 = nb0 + (c-1) small + k - 1).
 static __global__ void __launch_bounds__(256)
     k_ches_digits(const uint8_t *__restrict__ scalars, size_t stride, size_t n, int q_exp, int h,
                   const uint32_t *__restrict__ hash, uint32_t *__restrict__ keys, uint32_t *__restrict__ ranks,
-                  uint32_t *__restrict__ counts) {
+                  uint32_t *__restrict__ counts, uint32_t nb0, uint32_t small, uint32_t copies) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint8_t *sp = scalars + i * stride;
@@ -216,6 +218,13 @@ static __global__ void __launch_bounds__(256)
     carry = e >> 31;
     size_t k = i * (size_t)h + j;
     uint32_t b = e & CH_IDX_MASK;
+    if (j == h - 1 && b != 0 && b <= small) {
+      uint32_t c = (uint32_t)(i % copies);
+      if (c) {
+        b = nb0 + (c - 1) * small + b - 1;
+        e = (e & ~CH_IDX_MASK) | b;
+      }
+    }
     if (b) {
       ranks[k] = atomicAdd(&counts[b], 1u);
       keys[k] = e;
@@ -256,6 +265,37 @@ static __global__ void __launch_bounds__(256)
     }
   }
   st16(&dst[t], acc);
+}
+
+// ------------------------------------------------------- dense scan reduce --
+// suffix-scan step within each window of S: out[k] = in[k] + in[k + d] (k + d < S)
+template <int G>
+static __global__ void __launch_bounds__(64)
+    k_suffix_step(const Xyzz<typename FieldOf<G>::F> *__restrict__ in, Xyzz<typename FieldOf<G>::F> *__restrict__ out,
+                  int S, int d, int W) {
+  typedef typename FieldOf<G>::F F;
+  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (size_t)W * S) return;
+  int k = (int)(t % (size_t)S);
+  Xyzz<F> a = ld16(&in[t]);
+  if (k + d < S) {
+    Xyzz<F> b = ld16(&in[t + d]);
+    xyzz_add(a, b);
+  }
+  st16(&out[t], a);
+}
+// pairwise tree step: out[w*(S/2) + k] = in[w*S + 2k] + in[w*S + 2k + 1]
+template <int G>
+static __global__ void __launch_bounds__(64)
+    k_pair_step(const Xyzz<typename FieldOf<G>::F> *__restrict__ in, Xyzz<typename FieldOf<G>::F> *__restrict__ out,
+                size_t nout) {
+  typedef typename FieldOf<G>::F F;
+  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nout) return;
+  Xyzz<F> a = ld16(&in[2 * t]);
+  Xyzz<F> b = ld16(&in[2 * t + 1]);
+  xyzz_add(a, b);
+  st16(&out[t], a);
 }
 
 // blst xyzz {x, y, zzz, zz} (Montgomery R=2^384) -> internal xyzz

@@ -126,16 +126,34 @@ std::vector<int> ches_bucket_set(int q, int a_h);
 // packed digit hash (ches_kernels.hpp layout) of ref main_p1.cpp:140-152, q+1 entries
 std::vector<uint32_t> ches_digit_hash(const std::vector<int> &B, int q);
 
-// sum_{i >= 1} B[i] * S_i for ascending weights B (B[0] = 0) over device xyzz
-// buckets S (replaces ref multi_scalar.c:301-321).  Two regroupings by the low
-// and high halves of B[i] (2 xyzz adds per bucket) and one dense 2-window
-// reduction; the plan depends only on B and is built once.
+// Low-depth dense reduction: for each of W windows of S buckets (A[w*S + b-1]
+// holds bucket value b, S a power of two), T_w = sum_b b A_b computed as the sum
+// of all suffix sums: log2(S) Hillis-Steele suffix-scan steps + log2(S) pairwise
+// tree steps, one xyzz add per lane per step.  Depth 2 log2(S) adds (vs ~20
+// dependent adds per level of the running-sum recursion), which matters
+// because a lone dependent xyzz add costs ~15 us of one SIMD's issue time.
+template <int G>
+struct ScanReducer {
+  typedef typename HostField<G>::F HF;
+  DevBuf buf[2], fin;
+  void launch(hipStream_t s, const void *A, int W, int S);
+  void read(hipStream_t s, int W, std::vector<hfp::Jac<HF>> &out);
+
+ private:
+  int last_ = 0;
+};
+
+// sum_i w[i] * S_i for arbitrary non-negative bucket weights w (w = 0: bucket
+// ignored) over device xyzz buckets S (replaces ref multi_scalar.c:301-321).
+// Two regroupings by the low and high halves of w[i] (2 xyzz adds per bucket),
+// then a dense 2-window ScanReducer and one 2^s Horner step on the host.  The
+// plan depends only on w and is built once.
 template <int G>
 class WeightedReducer {
  public:
   typedef typename HostField<G>::F HF;
-  void plan(const std::vector<int> &B);
-  void launch(hipStream_t s, const void *S);   // device xyzz[|B|]
+  void plan(const std::vector<uint32_t> &w);
+  void launch(hipStream_t s, const void *S);   // device xyzz[w.size()]
   hfp::Jac<HF> read(hipStream_t s);             // waits
   size_t size() const { return bsize_; }
 
@@ -145,7 +163,7 @@ class WeightedReducer {
   DevBuf idx_, dense_buf_, part_[2];
   std::vector<DevBuf> starts_;
   std::vector<size_t> nout_;
-  DenseReducer<G> dense_;
+  ScanReducer<G> dense_;
 };
 
 template <int G>
@@ -164,7 +182,7 @@ class Ches {
   void run(hipStream_t s, const uint8_t *d_scalars, size_t stride, hfp::Jac<HF> *out);
   size_t npoints() const { return n_; }
   const ChesParams &params() const { return p_; }
-  size_t bucket_count() const { return B_.size(); }
+  size_t bucket_count() const { return B_.size() + (size_t)(copies_ - 1) * small_; }
   void set_profiling(bool on) { profile_ = on; }
   const PhaseTimes &times() const { return times_; }
   int device() const { return dev_; }
@@ -174,6 +192,11 @@ class Ches {
   ChesParams p_;
   std::vector<int> B_;
   size_t n_ = 0;
+  // top-digit bucket copies: the top MB digit is <= a_h + 1, so its n entries
+  // fall into the few buckets k <= small_ (B[k] <= a_h + 1); entry i of the top
+  // digit goes to copy i % copies_ of its bucket (copies share the weight B[k])
+  int small_ = 0, copies_ = 1;
+  void plan_buckets(size_t n);
   bool profile_ = false;
   PhaseTimes times_;
   DevBuf hash_, table_, keys_, ranks_, counts_, offsets_, sorted_, order_, iota_, sortkeys_, buckets_, tmp_;
