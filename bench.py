@@ -1,10 +1,13 @@
 #!/usr/bin/env python3
 """bench.py -- G1 MSM point-scalar pairs/s at n=2^20 per MI355X (BASELINE.json metric).
 
-One step = one complete G1 MSM over this rank's 2^20 fixed points with fresh
-scalars already resident in HBM (digits -> sort -> bucket accumulation ->
-bucket reduction -> window combine), plus, for N > 1, the single exchange of
-the partial sums (all_gather of 144-B Jacobians over RCCL) and their fold.
+One step = one complete G1 MSM over this rank's 2^20 fixed points with the
+scalars already resident in HBM, by the reference's CHES "nh + q/5" method
+(BASELINE.json configs[2]: q = 2^22, h = 12, |B| = 874 437, precomputed table
+T = m q^j P_i resident in HBM): MB digit conversion -> bucket sort -> bucket
+accumulation -> weighted bucket reduction, plus, for N > 1, the single exchange
+of the partial sums (all_gather of 144-B Jacobians over RCCL) and their fold.
+The plain Pippenger path (configs[1] method) is timed beside it (`methods`).
 Weak scaling: every GPU owns its own 2^20-point shard of the sequence
 P_i = 2^(i+1) G, so the job computes an MSM of N * 2^20 pairs per step.
 
@@ -15,8 +18,9 @@ Usage:
 Prints ONE JSON line on rank 0 with value = total pairs / (max-over-ranks
 time of K steps), a `roofline` object for the dominant kernel (bucket
 accumulation, timed with HIP events on the stream it runs on), and a
-`cpu_baseline` object (the CPU oracle port of the reference's blst Pippenger,
-1 thread, on a bounded prefix of the same workload; rank 0, N = 1 only).
+`cpu_baseline` object (the reference's own blst_p1s_mult_pippenger built from
+/root/reference into oracle/_ref, 1 thread, on the same points and scalars;
+rank 0, N = 1 only; the oracle port if that build is absent).
 """
 import argparse
 import json
@@ -31,12 +35,39 @@ METRIC = "G1 MSM point-scalar pairs/sec at n=2^20, 1/2/4/8 MI355X; bit-exact vs 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 VALU_PEAK_LANE_OPS = 78.6e12   # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (one VALU op / lane / clk)
 MADS_PER_FPMUL = 392           # 14x14 product + 14x14 reduction, one v_mad_u64_u32 each (fp.hpp)
-BYTES_PER_PAIR = 128           # 96 B affine point + 32 B scalar (SURVEY 8d, G1 plain)
+FPMUL_PEAK = 76.8e9            # measured register-resident Fp-mul/s, tools/microbench/fp_rate.hip (profiles/)
+AFFINE_BYTES = 96              # one G1 affine point (blst layout), SURVEY 8d
 FPMUL_PER_MADD = 10            # 8M + 2S (ec_ops.h:727-748)
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def timed_steps(step, ctx, steps, warmup, world, dev):
+    """W untimed + K timed steps bracketed by barrier + synchronize; max over ranks."""
+    import torch
+    for _ in range(warmup):
+        res = step()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize(dev)
+    acc_ms, tot_ms = [], []
+    t_start = time.perf_counter()
+    for _ in range(steps):
+        res = step()
+        ph = ctx.phase_times()
+        acc_ms.append(ph["accumulate"])
+        tot_ms.append(ph["total"])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return res, elapsed, acc_ms, tot_ms, ctx.phase_times()
 
 
 def main():
@@ -45,7 +76,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--log-n", type=int, default=20, help="points per GPU = 2^log_n")
-    ap.add_argument("--window", type=int, default=16)
+    ap.add_argument("--method", choices=("ches", "pippenger"), default="ches")
+    ap.add_argument("--window", type=int, default=16, help="plain Pippenger window bits")
+    ap.add_argument("--no-compare", action="store_true", help="skip timing the other method (N = 1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-log-n", type=int, default=20)
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
@@ -77,73 +110,89 @@ def main():
     pts = m.fixed_points(1, n, start)
     sc = m.gen_scalars(n, 1 + rank)
     log(f"[rank {rank}] inputs generated in {time.time() - t0:.1f}s (points {start}..{start + n})")
-
-    ctx = m.MSMContext(1, local, args.window)
     stream = torch.cuda.current_stream(dev)
-    ctx.set_points(pts, n, stream=stream.cuda_stream)
     d_sc = torch.frombuffer(bytearray(bytes(sc)), dtype=torch.uint8).to(dev)
-    torch.cuda.synchronize(dev)
-    ctx.set_profiling(True)
-
     add = mdist.engine_add(1)
 
-    def step():
-        part = ctx.mult(d_sc.data_ptr(), 255, stride=32, on_device=True, stream=stream.cuda_stream)
-        if world > 1:
-            return mdist.fold(mdist.gather_partials(part, 1, dev), add)
-        return part
+    def make(method):
+        t = time.time()
+        if method == "ches":
+            ctx = m.CHESContext(1, local, n_exp=args.log_n)
+            ctx.build_table(pts, n, stream=stream.cuda_stream)
 
-    for _ in range(args.warmup):
-        res = step()
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize(dev)
-    acc_ms, tot_ms = [], []
-    t_start = time.perf_counter()
-    for _ in range(args.steps):
-        res = step()
-        ph = ctx.phase_times()
-        acc_ms.append(ph["accumulate"])
-        tot_ms.append(ph["total"])
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        torch.distributed.barrier()
-    elapsed = time.perf_counter() - t_start
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
-    phases = ctx.phase_times()
+            def mult():
+                return ctx.mult(d_sc.data_ptr(), 32, on_device=True, stream=stream.cuda_stream)
+        else:
+            ctx = m.MSMContext(1, local, args.window)
+            ctx.set_points(pts, n, stream=stream.cuda_stream)
 
-    # parity of the timed result (N = 1: the reference's golden value for seed 1)
-    parity = None
-    if world == 1 and args.log_n == 20:
-        gold = json.load(open(os.path.join(REPO, "tests", "golden", "msm_g1.json")))
-        want = [c for c in gold["cases"] if c["n"] == n and c["seed"] == 1 and c["case"] == "rand"][0]["compressed"]
-        parity = m.compress(1, res).hex() == want
+            def mult():
+                return ctx.mult(d_sc.data_ptr(), 255, stride=32, on_device=True, stream=stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+        log(f"[rank {rank}] {method} setup {time.time() - t:.3f}s")
+        ctx.set_profiling(True)
+
+        def step():
+            part = mult()
+            if world > 1:
+                return mdist.fold(mdist.gather_partials(part, 1, dev), add)
+            return part
+        return ctx, step
+
+    ctx, step = make(args.method)
+    res, elapsed, acc_ms, tot_ms, phases = timed_steps(step, ctx, args.steps, args.warmup, world, dev)
+
+    gold = json.load(open(os.path.join(REPO, "tests", "golden", "msm_g1.json")))
+    want = [c["compressed"] for c in gold["cases"] if c["n"] == n and c["seed"] == 1 and c["case"] == "rand"]
+    parity = (m.compress(1, res).hex() == want[0]) if (world == 1 and want) else None
+
+    other = None
+    if world == 1 and not args.no_compare:
+        ometh = "pippenger" if args.method == "ches" else "ches"
+        octx, ostep = make(ometh)
+        ores, oel, oacc, _, oph = timed_steps(ostep, octx, max(5, args.steps // 2), 2, world, dev)
+        other = {"method": ometh, "value": round(n * max(5, args.steps // 2) / oel, 1), "unit": "pairs/s",
+                 "ms_per_step": round(oel / max(5, args.steps // 2) * 1e3, 4),
+                 "phases_ms": {k: round(v, 4) for k, v in oph.items()},
+                 "parity_vs_reference": (m.compress(1, ores).hex() == want[0]) if want else None}
+        octx.close()
 
     if rank != 0:
         if world > 1:
             torch.distributed.destroy_process_group()
         return
 
-    total_pairs = n * world * args.steps
-    value = total_pairs / elapsed
-    W = (255 + 1 + args.window - 1) // args.window
+    value = n * world * args.steps / elapsed
     acc_s = sum(acc_ms) / len(acc_ms) / 1e3
-    achieved_gbs = n * BYTES_PER_PAIR / acc_s / 1e9
+    if args.method == "ches":
+        h = ctx.params["h"]
+        madds = n * h                                 # one table point per (i, j) digit
+        alg_bytes = n * h * AFFINE_BYTES              # h affine gathers per pair (1184 B/pair incl. scalar)
+        workload = (f"G1 MSM n=2^{args.log_n} per GPU, CHES nh+q/5 (q=2^{ctx.params['q_exp']}, h={h}, "
+                    f"|B|={ctx.params['b_size']}), table T=m*q^j*P_i resident in HBM, scalars resident in HBM")
+        cfg_extra = {"method": "ches_q_over_5", "q_exp": ctx.params["q_exp"], "h": h,
+                     "bucket_set": ctx.params["b_size"], "buckets_incl_top_digit_copies": ctx.bucket_count()}
+    else:
+        W = (255 + 1 + args.window - 1) // args.window
+        madds = n * W
+        alg_bytes = n * (AFFINE_BYTES + 32)
+        workload = (f"G1 MSM n=2^{args.log_n} per GPU, plain Pippenger c={args.window} ({W} windows), "
+                    f"points+scalars resident in HBM")
+        cfg_extra = {"method": "pippenger", "window_bits": args.window}
+    achieved_gbs = alg_bytes / acc_s / 1e9
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
-            traffic = json.load(open(args.traffic_json)).get("accumulate_bytes_per_launch")
+            tj = json.load(open(args.traffic_json))
+            if tj.get("method") == args.method and tj.get("log_n") == args.log_n:
+                traffic = tj.get("accumulate_bytes_per_launch")
         except Exception:
             traffic = None
-    fpmul_rate = n * W * FPMUL_PER_MADD / acc_s
-    fpmul_peak = VALU_PEAK_LANE_OPS / MADS_PER_FPMUL
+    fpmul_rate = madds * FPMUL_PER_MADD / acc_s
 
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(m, pts, sc, args.cpu_sample_log_n, ctx_window=args.window)
+        cpu = cpu_baseline(m, pts, sc, args.cpu_sample_log_n)
 
     line = {
         "metric": METRIC,
@@ -158,23 +207,22 @@ def main():
         "vs_baseline": None,
         "dtype": "u32 (exact Fp381 integer arithmetic, 14x28-bit limbs)",
         "data": "synthetic: P_i = 2^(i+1) G1 (main_p1.cpp:52-66), SplitMix64 scalars < r (BASELINE.md sec.3)",
-        "config": {"workload": f"G1 MSM n=2^{args.log_n} per GPU, plain Pippenger c={args.window} "
-                               f"({W} windows), points+scalars resident in HBM",
-                   "n_per_gpu": n, "n_total": n * world, "method": "pippenger", "window_bits": args.window,
-                   "parallelism": f"points sharded x{world}, RCCL all_gather of partials"},
+        "config": dict({"workload": workload, "n_per_gpu": n, "n_total": n * world,
+                        "parallelism": f"points sharded x{world}, RCCL all_gather of 144-B partials"}, **cfg_extra),
         "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved_gbs / HBM_PEAK_GBS, 5), "traffic": traffic,
-                     "kernel": "k_accumulate (bucket accumulation)",
-                     "kernel_ms": round(acc_s * 1e3, 4),
-                     "algorithmic_bytes_per_launch": n * BYTES_PER_PAIR,
-                     "note": "kernel is VALU-integer bound, see valu_roofline"},
+                     "kernel": "k_accumulate (bucket accumulation)", "kernel_ms": round(acc_s * 1e3, 4),
+                     "algorithmic_bytes_per_launch": alg_bytes,
+                     "note": "integer-VALU bound (v_mad_u64_u32 issue), see valu_roofline"},
         "valu_roofline": {"bound": "valu-int", "achieved": round(fpmul_rate / 1e9, 2),
-                          "peak": round(fpmul_peak / 1e9, 2), "unit": "G Fp-mul/s",
-                          "frac": round(fpmul_rate / fpmul_peak, 4),
-                          "work": f"{W} windows x 10 Fp-mul per madd per pair",
-                          "peak_basis": "78.6T VALU lane-ops/s / 392 v_mad_u64_u32 per Fp-mul"},
+                          "peak": round(FPMUL_PEAK / 1e9, 2), "unit": "G Fp-mul/s",
+                          "frac": round(fpmul_rate / FPMUL_PEAK, 4),
+                          "work": f"{madds} xyzz madds x {FPMUL_PER_MADD} Fp-mul",
+                          "peak_basis": "measured register-resident Fp-mul kernel (tools/microbench/fp_rate.hip)"},
         "phases_ms": {k: round(v, 4) for k, v in phases.items()},
         "parity_vs_reference": parity,
+        "methods": {args.method: {"value": round(value, 1), "ms_per_step": round(elapsed / args.steps * 1e3, 4)},
+                    **({other["method"]: other} if other else {})},
         "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)
@@ -182,7 +230,7 @@ def main():
         torch.distributed.destroy_process_group()
 
 
-def cpu_baseline(m, pts, sc, log_n, ctx_window):
+def cpu_baseline(m, pts, sc, log_n):
     """The reference's own blst_p1s_mult_pippenger (libblst built from /root/reference
     sources into oracle/_ref/libblst_ref.so, x86-64 mulx asm), 1 thread -- the
     reference has no threading -- timed on this host's cores on the same points and
@@ -218,9 +266,9 @@ def cpu_baseline(m, pts, sc, log_n, ctx_window):
         r = of.msm(1, P, S, k, 255, "pippenger")
         dt = time.perf_counter() - t
         cpu_res, kind, what = of.compress(1, r), "port", "oracle port of blst Pippenger (oracle/msm_oracle.c)"
-    ctx = m.MSMContext(1, 0, ctx_window)
-    ctx.set_points(P, k)
-    gpu_res = m.compress(1, ctx.mult(S, 255)).hex()
+    ctx = m.CHESContext(1, 0, n_exp=log_n)
+    ctx.build_table(P, k)
+    gpu_res = m.compress(1, ctx.mult(S)).hex()
     ctx.close()
     return {"value": round(k / dt, 1), "unit": "pairs/s", "cores": 1, "kind": kind,
             "sample": f"{what}, 1 thread, first 2^{log_n} points/scalars of the rank-0 workload, {dt:.1f}s",

@@ -373,38 +373,21 @@ void Ches<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, hfp::J
   }
   const size_t n = n_, h = (size_t)p_.h, ne = n * h, NB = bucket_count();
   keys_.ensure(ne * 4);
-  ranks_.ensure(ne * 4);
+  vals_.ensure(ne * 4);
   sorted_.ensure(ne * 4);
   counts_.ensure(NB * 4);
   offsets_.ensure(NB * 4);
   order_.ensure(NB * 4);
-  iota_.ensure(NB * 4);
-  sortkeys_.ensure(NB * 4);
   buckets_.ensure(NB * sizeof(Xyzz<F>));
-  size_t scan_tmp = 0, sort_tmp = 0;
-  hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, counts_.as<uint32_t>(), offsets_.as<uint32_t>(), (int)NB, s);
-  int sort_bits = 1;  // counts <= ne
-  while (sort_bits < 32 && ((size_t)1 << sort_bits) <= ne) ++sort_bits;
-  hipcub::DeviceRadixSort::SortPairsDescending(nullptr, sort_tmp, counts_.as<uint32_t>(), sortkeys_.as<uint32_t>(),
-                                               iota_.as<uint32_t>(), order_.as<uint32_t>(), (int)NB, 0, sort_bits, s);
-  tmp_.ensure(std::max(scan_tmp, sort_tmp));
 
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[0], s));
-  MSM_HIP_CHECK(hipMemsetAsync(counts_.p, 0, NB * 4, s));
   hipLaunchKernelGGL(k_ches_digits, dim3(nblk(n, 256)), dim3(256), 0, s, d_scalars, stride, n, p_.q_exp, p_.h,
-                     hash_.as<uint32_t>(), keys_.as<uint32_t>(), ranks_.as<uint32_t>(), counts_.as<uint32_t>(),
-                     (uint32_t)B_.size(), (uint32_t)small_, (uint32_t)copies_);
+                     hash_.as<uint32_t>(), keys_.as<uint32_t>(), vals_.as<uint32_t>(), (uint32_t)B_.size(),
+                     (uint32_t)small_, (uint32_t)copies_);
   MSM_HIP_CHECK(hipGetLastError());
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[1], s));
-  size_t tb = tmp_.bytes;
-  MSM_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp_.p, tb, counts_.as<uint32_t>(), offsets_.as<uint32_t>(), (int)NB, s));
-  hipLaunchKernelGGL(k_ches_scatter, dim3(nblk(ne, 256)), dim3(256), 0, s, keys_.as<uint32_t>(), ranks_.as<uint32_t>(),
-                     offsets_.as<uint32_t>(), sorted_.as<uint32_t>(), ne);
-  hipLaunchKernelGGL(k_iota, dim3(nblk(NB, 256)), dim3(256), 0, s, iota_.as<uint32_t>(), NB);
-  tb = tmp_.bytes;
-  MSM_HIP_CHECK(hipcub::DeviceRadixSort::SortPairsDescending(tmp_.p, tb, counts_.as<uint32_t>(), sortkeys_.as<uint32_t>(),
-                                                             iota_.as<uint32_t>(), order_.as<uint32_t>(), (int)NB, 0,
-                                                             sort_bits, s));
+  sort_.run(s, keys_.as<uint32_t>(), vals_.as<uint32_t>(), ne, (uint32_t)NB, sorted_.as<uint32_t>(),
+            counts_.as<uint32_t>(), offsets_.as<uint32_t>(), order_.as<uint32_t>());
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[2], s));
   hipLaunchKernelGGL(k_accumulate<G>, dim3(nblk(NB, 256)), dim3(256), 0, s, order_.as<uint32_t>(),
                      counts_.as<uint32_t>(), offsets_.as<uint32_t>(), sorted_.as<uint32_t>(), table_.as<Aff<F>>(),

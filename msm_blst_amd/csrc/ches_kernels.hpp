@@ -10,8 +10,8 @@
 //                   q-ary digit + carry -> digit-hash lookup -> (bucket index,
 //                   m, alpha); entries with bucket value 0 are dropped (the
 //                   reference's `if (booth_idx)` guard, multi_scalar.c:440)
-//   k_ches_scatter  counting-sort placement of the (i, j) entries by bucket;
-//                   payload = table slot | sign << 31
+//                   -> one (bucket, table slot | sign << 31) entry per digit,
+//                   sorted by BucketSort (bucket_sort.hpp)
 //   k_segsum        segment sums of xyzz points over an index list (the two
 //                   regroupings of the bucket reduction, see ches.hip)
 // Bucket accumulation and the dense window reduction reuse k_accumulate /
@@ -188,8 +188,8 @@ __device__ __forceinline__ void sub_r_if_ge(uint32_t s[8]) {
 // bucket k (copy 0 = k itself, copy c >= 1 = nb0 + (c-1) small + k - 1).
 static __global__ void __launch_bounds__(256)
     k_ches_digits(const uint8_t *__restrict__ scalars, size_t stride, size_t n, int q_exp, int h,
-                  const uint32_t *__restrict__ hash, uint32_t *__restrict__ keys, uint32_t *__restrict__ ranks,
-                  uint32_t *__restrict__ counts, uint32_t nb0, uint32_t small, uint32_t copies) {
+                  const uint32_t *__restrict__ hash, uint32_t *__restrict__ keys, uint32_t *__restrict__ vals,
+                  uint32_t nb0, uint32_t small, uint32_t copies) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint8_t *sp = scalars + i * stride;
@@ -220,28 +220,15 @@ static __global__ void __launch_bounds__(256)
     uint32_t b = e & CH_IDX_MASK;
     if (j == h - 1 && b != 0 && b <= small) {
       uint32_t c = (uint32_t)(i % copies);
-      if (c) {
-        b = nb0 + (c - 1) * small + b - 1;
-        e = (e & ~CH_IDX_MASK) | b;
-      }
+      if (c) b = nb0 + (c - 1) * small + b - 1;
     }
     if (b) {
-      ranks[k] = atomicAdd(&counts[b], 1u);
-      keys[k] = e;
+      keys[k] = b;
+      vals[k] = (uint32_t)(3 * k + ((e >> 24) & 3u)) | (e & 0x80000000u);
     } else {
       keys[k] = KEY_NONE;
     }
   }
-}
-
-static __global__ void k_ches_scatter(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ ranks,
-                               const uint32_t *__restrict__ offsets, uint32_t *__restrict__ sorted, size_t ne) {
-  size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= ne) return;
-  uint32_t k = keys[e];
-  if (k == KEY_NONE) return;
-  uint32_t b = k & CH_IDX_MASK, m1 = (k >> 24) & 3u;
-  sorted[offsets[b] + ranks[e]] = (uint32_t)(3 * e + m1) | (k & 0x80000000u);
 }
 
 // ------------------------------------------------------------ segment sums --

@@ -3,6 +3,9 @@
 // stream; the only host synchronisation is the final 16-window read-back.
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+
+#include "bucket_sort.hpp"
 #include "engine.hpp"
 #include "kernels.hpp"
 
@@ -13,6 +16,46 @@
 #endif
 
 namespace msm {
+
+#if MSM_GROUP == 1  // group-independent: compiled once
+void BucketSort::run(hipStream_t s, const uint32_t *keys, const uint32_t *vals, size_t ne, uint32_t nb,
+                     uint32_t *sorted, uint32_t *counts, uint32_t *offsets, uint32_t *order) {
+  const int ncb = (int)((nb + (1u << BS_FB_BITS) - 1) >> BS_FB_BITS);
+  if (ncb > BS_MAX_CB) throw std::runtime_error("BucketSort: too many buckets");
+  if (ne >= (1ull << 32)) throw std::runtime_error("BucketSort: too many entries");
+  const int ntiles = (int)std::max<size_t>(1, (ne + BS_TILE - 1) / BS_TILE);
+  const size_t nslots = (size_t)ncb * ntiles;
+  ghist.ensure(nslots * 4);
+  gbase.ensure(nslots * 4);
+  okeys.ensure(std::max<size_t>(ne, 1) * 4);
+  ovals.ensure(std::max<size_t>(ne, 1) * 4);
+  total.ensure(16);
+  sched.ensure((size_t)nb * 4);
+  iota.ensure((size_t)nb * 4);
+  size_t scan_tmp = 0, sort_tmp = 0;
+  hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, ghist.as<uint32_t>(), gbase.as<uint32_t>(), (int)nslots, s);
+  hipcub::DeviceRadixSort::SortPairsDescending(nullptr, sort_tmp, sched.as<uint32_t>(), sched.as<uint32_t>(),
+                                               iota.as<uint32_t>(), order, (int)nb, 0, 8, s);
+  tmp.ensure(std::max(scan_tmp, sort_tmp) + (size_t)nb * 4);
+  uint32_t *sched_sorted = reinterpret_cast<uint32_t *>(tmp.as<uint8_t>() + std::max(scan_tmp, sort_tmp));
+  hipLaunchKernelGGL(k_bs_hist, dim3(ntiles), dim3(256), 0, s, keys, ne, ncb, ntiles, ghist.as<uint32_t>());
+  MSM_HIP_CHECK(hipGetLastError());
+  size_t tb = scan_tmp;
+  MSM_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, ghist.as<uint32_t>(), gbase.as<uint32_t>(), (int)nslots, s));
+  hipLaunchKernelGGL(k_bs_total, dim3(1), dim3(64), 0, s, gbase.as<uint32_t>(), ghist.as<uint32_t>(), nslots,
+                     total.as<uint32_t>());
+  hipLaunchKernelGGL(k_bs_coarse, dim3(ntiles), dim3(256), 0, s, keys, vals, ne, ncb, ntiles, gbase.as<uint32_t>(),
+                     okeys.as<uint32_t>(), ovals.as<uint32_t>());
+  MSM_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(k_bs_fine, dim3(ncb), dim3(512), 0, s, okeys.as<uint32_t>(), ovals.as<uint32_t>(), ncb, ntiles,
+                     gbase.as<uint32_t>(), total.as<uint32_t>(), nb, sorted, counts, offsets, sched.as<uint32_t>());
+  MSM_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(k_iota, dim3(nblk(nb, 256)), dim3(256), 0, s, iota.as<uint32_t>(), (size_t)nb);
+  tb = sort_tmp;
+  MSM_HIP_CHECK(hipcub::DeviceRadixSort::SortPairsDescending(tmp.p, tb, sched.as<uint32_t>(), sched_sorted,
+                                                             iota.as<uint32_t>(), order, (int)nb, 0, 8, s));
+}
+#endif
 
 
 template <int G>
@@ -52,13 +95,8 @@ void Pippenger<G>::set_points(const void *pts, size_t n, bool on_device, hipStre
 
 template <int C>
 static void launch_digits(hipStream_t s, const uint8_t *sc, size_t stride, size_t n, int nbits, int W, uint32_t *keys,
-                          uint32_t *ranks, uint32_t *counts) {
-  hipLaunchKernelGGL(k_digits<C>, dim3(nblk(n, 256)), dim3(256), 0, s, sc, stride, n, nbits, W, keys, ranks, counts);
-}
-template <int C>
-static void launch_scatter(hipStream_t s, const uint32_t *keys, const uint32_t *ranks, const uint32_t *off,
-                           uint32_t *sorted, size_t n, int W) {
-  hipLaunchKernelGGL(k_scatter<C>, dim3(nblk((size_t)W * n, 256)), dim3(256), 0, s, keys, ranks, off, sorted, n, W);
+                          uint32_t *vals) {
+  hipLaunchKernelGGL(k_digits<C>, dim3(nblk(n, 256)), dim3(256), 0, s, sc, stride, n, nbits, W, keys, vals);
 }
 
 #define MSM_C_DISPATCH(c, FN, ...)                          \
@@ -92,38 +130,21 @@ void Pippenger<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, i
     *out = ret;
     return;
   }
-  const size_t n = n_;
-  keys_.ensure((size_t)W * n * 4);
-  ranks_.ensure((size_t)W * n * 4);
-  sorted_.ensure((size_t)W * n * 4);
+  const size_t n = n_, ne = (size_t)W * n;
+  keys_.ensure(ne * 4);
+  vals_.ensure(ne * 4);
+  sorted_.ensure(ne * 4);
   counts_.ensure(NT * 4);
   offsets_.ensure(NT * 4);
   order_.ensure(NT * 4);
-  iota_.ensure(NT * 4);
-  sortkeys_.ensure(NT * 4);
   buckets_.ensure(NT * sizeof(Xyzz<F>));
 
-  size_t scan_tmp = 0, sort_tmp = 0;
-  hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, counts_.as<uint32_t>(), offsets_.as<uint32_t>(), (int)NT, s);
-  hipcub::DeviceRadixSort::SortPairsDescending(nullptr, sort_tmp, counts_.as<uint32_t>(), sortkeys_.as<uint32_t>(),
-                                               iota_.as<uint32_t>(), order_.as<uint32_t>(), (int)NT, 0, 32, s);
-  tmp_.ensure(scan_tmp > sort_tmp ? scan_tmp : sort_tmp);
-
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[0], s));
-  MSM_HIP_CHECK(hipMemsetAsync(counts_.p, 0, NT * 4, s));
-  MSM_C_DISPATCH(c, launch_digits, s, d_scalars, stride, n, nbits, W, keys_.as<uint32_t>(), ranks_.as<uint32_t>(),
-                 counts_.as<uint32_t>());
+  MSM_C_DISPATCH(c, launch_digits, s, d_scalars, stride, n, nbits, W, keys_.as<uint32_t>(), vals_.as<uint32_t>());
   MSM_HIP_CHECK(hipGetLastError());
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[1], s));
-  size_t tb = tmp_.bytes;
-  MSM_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp_.p, tb, counts_.as<uint32_t>(), offsets_.as<uint32_t>(), (int)NT, s));
-  MSM_C_DISPATCH(c, launch_scatter, s, keys_.as<uint32_t>(), ranks_.as<uint32_t>(), offsets_.as<uint32_t>(),
-                 sorted_.as<uint32_t>(), n, W);
-  hipLaunchKernelGGL(k_iota, dim3(nblk(NT, 256)), dim3(256), 0, s, iota_.as<uint32_t>(), NT);
-  tb = tmp_.bytes;
-  MSM_HIP_CHECK(hipcub::DeviceRadixSort::SortPairsDescending(tmp_.p, tb, counts_.as<uint32_t>(), sortkeys_.as<uint32_t>(),
-                                                             iota_.as<uint32_t>(), order_.as<uint32_t>(), (int)NT, 0, 32,
-                                                             s));
+  sort_.run(s, keys_.as<uint32_t>(), vals_.as<uint32_t>(), ne, (uint32_t)NT, sorted_.as<uint32_t>(),
+            counts_.as<uint32_t>(), offsets_.as<uint32_t>(), order_.as<uint32_t>());
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[2], s));
   hipLaunchKernelGGL(k_accumulate<G>, dim3(nblk(NT, 256)), dim3(256), 0, s, order_.as<uint32_t>(),
                      counts_.as<uint32_t>(), offsets_.as<uint32_t>(), sorted_.as<uint32_t>(), pts_.as<Aff<F>>(),

@@ -63,6 +63,16 @@ struct HostField<2> {
   typedef hfp::Fp2 F;
 };
 
+// Two-level LDS counting sort of (bucket, payload) entries (bucket_sort.hpp).
+// Produces payloads grouped by bucket, per-bucket counts/offsets and the
+// accumulation schedule: bucket ids ordered by count, descending (8-bit key).
+struct BucketSort {
+  DevBuf ghist, gbase, okeys, ovals, total, sched, iota, tmp;
+  // keys[ne] (bucket < nb or 0xffffffff), vals[ne]; outputs sized ne / nb
+  void run(hipStream_t s, const uint32_t *keys, const uint32_t *vals, size_t ne, uint32_t nb, uint32_t *sorted,
+           uint32_t *counts, uint32_t *offsets, uint32_t *order);
+};
+
 // Dense windowed bucket reduction: for each of W windows of S buckets
 // (A[w*S + b-1] holds bucket value b), T_w = sum_b b * A_b, read back to host
 // as blst Jacobians.  Shared by the Pippenger and CHES pipelines.
@@ -108,7 +118,8 @@ class Pippenger {
   size_t n_ = 0;
   bool profile_ = false;
   PhaseTimes times_;
-  DevBuf pts_, keys_, ranks_, counts_, offsets_, sorted_, order_, iota_, sortkeys_, buckets_, tmp_;
+  DevBuf pts_, keys_, vals_, counts_, offsets_, sorted_, order_, buckets_, tmp_;
+  BucketSort sort_;
   DenseReducer<G> dense_;
   std::vector<hipEvent_t> ev_;
 };
@@ -199,7 +210,8 @@ class Ches {
   void plan_buckets(size_t n);
   bool profile_ = false;
   PhaseTimes times_;
-  DevBuf hash_, table_, keys_, ranks_, counts_, offsets_, sorted_, order_, iota_, sortkeys_, buckets_, tmp_;
+  DevBuf hash_, table_, keys_, vals_, counts_, offsets_, sorted_, order_, buckets_;
+  BucketSort sort_;
   WeightedReducer<G> red_;
   std::vector<hipEvent_t> ev_;
 };

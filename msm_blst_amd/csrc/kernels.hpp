@@ -3,11 +3,11 @@
 //
 // Plain Pippenger pipeline (replaces ref src/multi_scalar.c:383-419 tile /
 // :281-297 integrate / :549-576 window loop):
-//   k_digits      signed c-bit window digits of every scalar, per-bucket
-//                 histogram (atomics) + each entry's rank within its bucket
-//   k_scatter     counting-sort placement: sorted[off[bucket] + rank] = point
-//   (hipcub)      exclusive scan of counts; bucket schedule = ids sorted by
-//                 count, descending, so a wavefront's 64 buckets are equally long
+//   k_digits      signed c-bit window digits of every scalar -> one (bucket,
+//                 point | sign) entry per window
+//   BucketSort    two-level LDS counting sort by bucket (bucket_sort.hpp);
+//                 bucket schedule = ids sorted by count, descending, so a
+//                 wavefront's 64 buckets are equally long
 //   k_accumulate  one lane per bucket: xyzz += +-P over its sorted points
 //   k_reduce      segmented running sums, log_L(NB) levels (sum_b b*B_b)
 //   k_finalize    window totals -> blst Jacobian (R=2^384 Montgomery)
@@ -140,7 +140,7 @@ __device__ __forceinline__ uint32_t scalar_bits(const uint32_t s[10], int off, i
 
 template <int C>
 __global__ void k_digits(const uint8_t *__restrict__ scalars, size_t stride, size_t n, int nbits, int W,
-                         uint32_t *__restrict__ keys, uint32_t *__restrict__ ranks, uint32_t *__restrict__ counts) {
+                         uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   constexpr uint32_t NB = 1u << (C - 1);
@@ -183,27 +183,13 @@ __global__ void k_digits(const uint8_t *__restrict__ scalars, size_t stride, siz
       }
       size_t e = (size_t)w * n + i;
       if (b) {
-        uint32_t bi = b - 1;
-        ranks[e] = atomicAdd(&counts[(size_t)w * NB + bi], 1u);
-        keys[e] = bi | (sign << 31);
+        keys[e] = (uint32_t)w * NB + (b - 1);
+        vals[e] = (uint32_t)i | (sign << 31);
       } else {
         keys[e] = KEY_NONE;
       }
     }
   }
-}
-
-template <int C>
-__global__ void k_scatter(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ ranks,
-                          const uint32_t *__restrict__ offsets, uint32_t *__restrict__ sorted, size_t n, int W) {
-  size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= (size_t)W * n) return;
-  uint32_t k = keys[e];
-  if (k == KEY_NONE) return;
-  constexpr uint32_t NB = 1u << (C - 1);
-  size_t w = e / n, i = e - w * n;
-  uint32_t pos = offsets[w * NB + (k & 0x7fffffffu)] + ranks[e];
-  sorted[pos] = (uint32_t)i | (k & 0x80000000u);
 }
 
 static __global__ void k_iota(uint32_t *a, size_t n) {
