@@ -2,120 +2,231 @@
 //
 // Input: one (key, val) per entry, key = bucket id < NB (or KEY_NONE = skip),
 // val = payload (point/table slot | sign << 31).  Output: vals grouped by
-// bucket, per-bucket counts and offsets, and a schedule key per bucket.
-// All counting is in LDS; global memory only sees streaming reads and writes
-// that are contiguous per (tile, coarse bin) or within one coarse bin:
+// bucket and per-bucket counts and offsets.  All counting is in LDS; global
+// memory only sees streaming reads and writes that are contiguous per
+// (tile, coarse bin) or confined to one coarse bin's range:
 //
 //   k_bs_hist     per tile of TILE entries: LDS histogram over coarse bins
-//                 (bucket >> FB_BITS) -> ghist[bin * ntiles + tile]
+//                 (bucket >> fb_bits) -> ghist[bin * ntiles + tile]
 //   (hipcub)      exclusive scan of ghist (bin-major) -> gbase
 //   k_bs_coarse   per tile: LDS rank within (tile, bin) -> coarse-sorted keys/vals
-//   k_bs_fine     one workgroup per coarse bin: LDS histogram over its 2^FB_BITS
-//                 buckets, scan, counts/offsets out, scatter vals in bucket order
+//   k_bs_fine     one 1024-thread workgroup per coarse bin: LDS histogram over
+//                 its 2^fb_bits buckets, block scan, counts/offsets out, scatter
+//                 vals in bucket order (writes stay inside the bin's range)
 //
-// Replaces the random-address global atomicAdd ranks of the first engine
-// (~20 G atomics/s chip-wide, MI355X_MICROARCH.md "64 lanes in 64 different rows").
+// fb_bits is chosen per problem so that there are ~256 coarse bins: few enough
+// that a tile's writes to one bin form runs of tens of entries (the L2 merges
+// them), many enough to fill the chip in k_bs_fine.  Replaces the random-
+// address global atomicAdd ranks of the first engine (~20 G atomics/s
+// chip-wide, MI355X_MICROARCH.md "64 lanes in 64 different rows").
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace msm {
 
-constexpr int BS_TILE = 8192;      // entries per tile (256 threads x 32)
-constexpr int BS_FB_BITS = 10;     // fine buckets per coarse bin = 1024
-constexpr int BS_MAX_CB = 8192;    // coarse bins held in LDS (32 KiB): NB <= 2^23
+constexpr int BS_TILE = 8192;         // entries per tile (256 threads x 32)
+constexpr int BS_MAX_FB_BITS = 12;    // fine buckets per coarse bin <= 4096 (2 x 16 KiB LDS)
+constexpr int BS_MAX_CB = 8192;       // coarse bins held in LDS (32 KiB)
 constexpr uint32_t BS_NONE = 0xffffffffu;
 
 static __global__ void __launch_bounds__(256)
-    k_bs_hist(const uint32_t *__restrict__ keys, size_t ne, int ncb, int ntiles, uint32_t *__restrict__ ghist) {
+    k_bs_hist(const uint32_t *__restrict__ keys, size_t ne, int fb_bits, int ncb, int ntiles,
+              uint32_t *__restrict__ ghist) {
   __shared__ uint32_t h[BS_MAX_CB];
   for (int b = threadIdx.x; b < ncb; b += blockDim.x) h[b] = 0;
   __syncthreads();
   const size_t t0 = (size_t)blockIdx.x * BS_TILE;
-  const size_t t1 = t0 + BS_TILE < ne ? t0 + BS_TILE : ne;
-  for (size_t e = t0 + threadIdx.x; e < t1; e += blockDim.x) {
-    uint32_t k = keys[e];
-    if (k != BS_NONE) atomicAdd(&h[k >> BS_FB_BITS], 1u);
+  uint32_t kk[BS_TILE / 256];  // all of this thread's keys in flight at once
+#pragma unroll
+  for (int r = 0; r < BS_TILE / 256; ++r) {
+    size_t e = t0 + threadIdx.x + (size_t)r * 256;
+    kk[r] = e < ne ? keys[e] : BS_NONE;
   }
+#pragma unroll
+  for (int r = 0; r < BS_TILE / 256; ++r)
+    if (kk[r] != BS_NONE) atomicAdd(&h[kk[r] >> fb_bits], 1u);
   __syncthreads();
   for (int b = threadIdx.x; b < ncb; b += blockDim.x) ghist[(size_t)b * ntiles + blockIdx.x] = h[b];
 }
 
 static __global__ void __launch_bounds__(256)
-    k_bs_coarse(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ vals, size_t ne, int ncb, int ntiles,
-                const uint32_t *__restrict__ gbase, uint32_t *__restrict__ okeys, uint32_t *__restrict__ ovals) {
+    k_bs_coarse(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ vals, size_t ne, int fb_bits,
+                int ncb, int ntiles, const uint32_t *__restrict__ gbase, uint32_t *__restrict__ okeys,
+                uint32_t *__restrict__ ovals) {
   __shared__ uint32_t cur[BS_MAX_CB];
   for (int b = threadIdx.x; b < ncb; b += blockDim.x) cur[b] = gbase[(size_t)b * ntiles + blockIdx.x];
   __syncthreads();
   const size_t t0 = (size_t)blockIdx.x * BS_TILE;
-  const size_t t1 = t0 + BS_TILE < ne ? t0 + BS_TILE : ne;
-  for (size_t e = t0 + threadIdx.x; e < t1; e += blockDim.x) {
-    uint32_t k = keys[e];
-    if (k == BS_NONE) continue;
-    uint32_t pos = atomicAdd(&cur[k >> BS_FB_BITS], 1u);
-    okeys[pos] = k;
-    ovals[pos] = vals[e];
+  constexpr int R = BS_TILE / 256;
+  uint32_t kk[R], vv[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    size_t e = t0 + threadIdx.x + (size_t)r * 256;
+    kk[r] = e < ne ? keys[e] : BS_NONE;
+    vv[r] = e < ne ? vals[e] : 0u;
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    if (kk[r] == BS_NONE) continue;
+    uint32_t pos = atomicAdd(&cur[kk[r] >> fb_bits], 1u);
+    okeys[pos] = kk[r];
+    ovals[pos] = vv[r];
   }
 }
 
-// bin b covers buckets [b << FB_BITS, (b+1) << FB_BITS) and coarse-sorted
+// exclusive scan of a[0..n) in LDS by a 1024-thread block (n <= 4096); returns via a
+__device__ __forceinline__ void block_exclusive_scan_4096(uint32_t *a, int n, uint32_t *wsum) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int per = (n + 1023) / 1024;  // <= 4 consecutive elements per thread
+  uint32_t loc[4], s = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    int i = t * per + k;
+    loc[k] = s;
+    if (k < per && i < n) s += a[i];
+  }
+  uint32_t incl = s;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t v = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += v;
+  }
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  if (t == 0) {
+    uint32_t run = 0;
+    for (int w = 0; w < 16; ++w) {
+      uint32_t x = wsum[w];
+      wsum[w] = run;
+      run += x;
+    }
+  }
+  __syncthreads();
+  const uint32_t base = wsum[wave] + incl - s;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    int i = t * per + k;
+    if (k < per && i < n) a[i] = base + loc[k];
+  }
+  __syncthreads();
+}
+
+// bin b covers buckets [b << fb_bits, (b+1) << fb_bits) and coarse-sorted
 // entries [gbase[b * ntiles], end_b) where end_b = gbase[(b+1) * ntiles] or total.
-// sched_key[bucket] = min(count, 255) (the accumulation schedule sorts by it).
-static __global__ void __launch_bounds__(512)
-    k_bs_fine(const uint32_t *__restrict__ okeys, const uint32_t *__restrict__ ovals, int ncb, int ntiles,
-              const uint32_t *__restrict__ gbase, const uint32_t *__restrict__ total, uint32_t nb,
-              uint32_t *__restrict__ sorted, uint32_t *__restrict__ counts, uint32_t *__restrict__ offsets,
-              uint32_t *__restrict__ sched_key) {
-  constexpr int FB = 1 << BS_FB_BITS;
-  __shared__ uint32_t cnt[FB];
-  __shared__ uint32_t off[FB];
+static __global__ void __launch_bounds__(1024)
+    k_bs_fine(const uint32_t *__restrict__ okeys, const uint32_t *__restrict__ ovals, int fb_bits, int ncb,
+              int ntiles, const uint32_t *__restrict__ gbase, const uint32_t *__restrict__ total, uint32_t nb,
+              uint32_t *__restrict__ sorted, uint32_t *__restrict__ counts, uint32_t *__restrict__ offsets) {
+  __shared__ uint32_t cnt[1 << BS_MAX_FB_BITS];
+  __shared__ uint32_t off[1 << BS_MAX_FB_BITS];
+  __shared__ uint32_t wsum[16];
+  const int FB = 1 << fb_bits;
+  const uint32_t fmask = (uint32_t)FB - 1u;
   const int b = blockIdx.x;
   const uint32_t lo = gbase[(size_t)b * ntiles];
   const uint32_t hi = b + 1 < ncb ? gbase[(size_t)(b + 1) * ntiles] : *total;
   for (int f = threadIdx.x; f < FB; f += blockDim.x) cnt[f] = 0;
   __syncthreads();
-  for (uint32_t e = lo + threadIdx.x; e < hi; e += blockDim.x) atomicAdd(&cnt[okeys[e] & (FB - 1)], 1u);
-  __syncthreads();
-  // exclusive scan of cnt[0..FB) by one wave (FB = 1024 = 16 per lane)
-  if (threadIdx.x < 64) {
-    const int l = threadIdx.x;
-    uint32_t loc[FB / 64], s = 0;
+  constexpr int U = 8;  // loads in flight per thread
+  for (uint32_t e0 = lo; e0 < hi; e0 += U * 1024) {
+    uint32_t kk[U];
 #pragma unroll
-    for (int k = 0; k < FB / 64; ++k) {
-      loc[k] = s;
-      s += cnt[l * (FB / 64) + k];
+    for (int r = 0; r < U; ++r) {
+      uint32_t e = e0 + threadIdx.x + r * 1024;
+      kk[r] = e < hi ? okeys[e] : BS_NONE;
     }
-    uint32_t incl = s;  // wave-inclusive scan of the per-lane totals
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      uint32_t v = __shfl_up(incl, d, 64);
-      if (l >= d) incl += v;
-    }
-    uint32_t base = incl - s;
-#pragma unroll
-    for (int k = 0; k < FB / 64; ++k) off[l * (FB / 64) + k] = base + loc[k];
+    for (int r = 0; r < U; ++r)
+      if (kk[r] != BS_NONE) atomicAdd(&cnt[kk[r] & fmask], 1u);
   }
   __syncthreads();
+  for (int f = threadIdx.x; f < FB; f += blockDim.x) off[f] = cnt[f];
+  __syncthreads();
+  block_exclusive_scan_4096(off, FB, wsum);
   for (int f = threadIdx.x; f < FB; f += blockDim.x) {
-    uint32_t bucket = ((uint32_t)b << BS_FB_BITS) + f;
+    uint32_t bucket = ((uint32_t)b << fb_bits) + f;
     if (bucket < nb) {
-      uint32_t c = cnt[f];
-      counts[bucket] = c;
+      counts[bucket] = cnt[f];
       offsets[bucket] = lo + off[f];
-      sched_key[bucket] = c < 255u ? c : 255u;
     }
   }
   __syncthreads();
-  for (uint32_t e = lo + threadIdx.x; e < hi; e += blockDim.x) {
-    uint32_t k = okeys[e];
-    uint32_t pos = atomicAdd(&off[k & (FB - 1)], 1u);
-    sorted[lo + pos] = ovals[e];
+  for (uint32_t e0 = lo; e0 < hi; e0 += U * 1024) {
+    uint32_t kk[U], vv[U];
+#pragma unroll
+    for (int r = 0; r < U; ++r) {
+      uint32_t e = e0 + threadIdx.x + r * 1024;
+      kk[r] = e < hi ? okeys[e] : BS_NONE;
+      vv[r] = e < hi ? ovals[e] : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < U; ++r) {
+      if (kk[r] == BS_NONE) continue;
+      uint32_t pos = atomicAdd(&off[kk[r] & fmask], 1u);
+      sorted[lo + pos] = vv[r];
+    }
   }
 }
 
+// ---- accumulation schedule: bucket ids ordered by entry count, descending ----
+// class = 255 - min(count, 255).  k_sched_hist: per-class totals (LDS histogram
+// per 256 buckets, one global atomic per non-empty class).  k_sched_scatter:
+// each workgroup reserves its per-class ranges with one global atomic per class
+// and writes its bucket ids.  The order inside a class is arbitrary.
+static __global__ void __launch_bounds__(256)
+    k_sched_hist(const uint32_t *__restrict__ counts, uint32_t nb, uint32_t *__restrict__ class_total) {
+  __shared__ uint32_t h[256];
+  const uint32_t t = threadIdx.x, b = blockIdx.x * 256 + t;
+  h[t] = 0;
+  __syncthreads();
+  if (b < nb) {
+    uint32_t c = counts[b];
+    atomicAdd(&h[255u - (c < 255u ? c : 255u)], 1u);
+  }
+  __syncthreads();
+  if (h[t]) atomicAdd(&class_total[t], h[t]);
+}
+// class_total -> exclusive class bases, in place (one wave)
+static __global__ void k_sched_scan(uint32_t *__restrict__ class_total) {
+  const int l = threadIdx.x;
+  uint32_t v0 = class_total[4 * l], v1 = class_total[4 * l + 1], v2 = class_total[4 * l + 2],
+           v3 = class_total[4 * l + 3];
+  uint32_t s = v0 + v1 + v2 + v3, incl = s;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t v = __shfl_up(incl, d, 64);
+    if (l >= d) incl += v;
+  }
+  uint32_t base = incl - s;
+  class_total[4 * l] = base;
+  class_total[4 * l + 1] = base + v0;
+  class_total[4 * l + 2] = base + v0 + v1;
+  class_total[4 * l + 3] = base + v0 + v1 + v2;
+}
+static __global__ void __launch_bounds__(256)
+    k_sched_scatter(const uint32_t *__restrict__ counts, uint32_t nb, uint32_t *__restrict__ class_cursor,
+                    uint32_t *__restrict__ order) {
+  __shared__ uint32_t h[256];
+  __shared__ uint32_t base[256];
+  const uint32_t t = threadIdx.x, b = blockIdx.x * 256 + t;
+  h[t] = 0;
+  __syncthreads();
+  uint32_t cls = 0, rank = 0;
+  if (b < nb) {
+    uint32_t c = counts[b];
+    cls = 255u - (c < 255u ? c : 255u);
+    rank = atomicAdd(&h[cls], 1u);
+  }
+  __syncthreads();
+  if (h[t]) base[t] = atomicAdd(&class_cursor[t], h[t]);
+  __syncthreads();
+  if (b < nb) order[base[cls] + rank] = b;
+}
+
 // total number of valid entries = inclusive end of the last (bin, tile) slot
-static __global__ void k_bs_total(const uint32_t *__restrict__ gbase, const uint32_t *__restrict__ ghist, size_t nslots,
-                           uint32_t *__restrict__ total) {
+static __global__ void k_bs_total(const uint32_t *__restrict__ gbase, const uint32_t *__restrict__ ghist,
+                                  size_t nslots, uint32_t *__restrict__ total) {
   if (threadIdx.x == 0 && blockIdx.x == 0) *total = gbase[nslots - 1] + ghist[nslots - 1];
 }
 

@@ -145,9 +145,11 @@ template struct ScanReducer<MSM_GROUP>;
 // then a dense scatter into 2 windows of 2^s slots), followed by the dense
 // 2-window ScanReducer and a 2^s Horner step on the host.
 template <int G>
-void WeightedReducer<G>::plan(const std::vector<uint32_t> &w) {
+void WeightedReducer<G>::plan(const std::vector<uint32_t> &w, const std::vector<uint32_t> &win, int nwin) {
   typedef typename FieldOf<G>::F F;
+  if (nwin < 1 || (!win.empty() && win.size() != w.size())) throw std::runtime_error("WeightedReducer: bad windows");
   bsize_ = w.size();
+  nwin_ = nwin;
   starts_.clear();
   nout_.clear();
   uint32_t maxw = 0;
@@ -156,17 +158,22 @@ void WeightedReducer<G>::plan(const std::vector<uint32_t> &w) {
   while (bits < 32 && ((uint64_t)1 << bits) <= maxw) ++bits;
   sbits_ = std::max(1, (bits + 1) / 2);
   const uint32_t S = 1u << sbits_;
-  std::vector<std::vector<uint32_t>> byv(S), byu(S);
+  // dense slot layout: window ww -> [L block (2 ww) S | H block (2 ww + 1) S]
+  std::vector<std::vector<uint32_t>> byv((size_t)nwin * S), byu((size_t)nwin * S);
   for (size_t i = 0; i < w.size(); ++i) {
+    const size_t ww = win.empty() ? 0 : win[i];
+    if (ww >= (size_t)nwin) throw std::runtime_error("WeightedReducer: window out of range");
     uint32_t v = w[i] >> sbits_, u = w[i] & (S - 1);
-    if (v) byv[v].push_back((uint32_t)i);
-    if (u) byu[u].push_back((uint32_t)i);
+    if (v) byv[ww * S + v].push_back((uint32_t)i);
+    if (u) byu[ww * S + u].push_back((uint32_t)i);
   }
   std::vector<uint32_t> idx, seg;
-  for (uint32_t v = 1; v < S; ++v)
-    for (uint32_t i : byv[v]) idx.push_back(i), seg.push_back(S + v - 1);
-  for (uint32_t u = 1; u < S; ++u)
-    for (uint32_t i : byu[u]) idx.push_back(i), seg.push_back(u - 1);
+  for (int ww = 0; ww < nwin; ++ww) {
+    for (uint32_t v = 1; v < S; ++v)
+      for (uint32_t i : byv[(size_t)ww * S + v]) idx.push_back(i), seg.push_back((2 * ww + 1) * S + v - 1);
+    for (uint32_t u = 1; u < S; ++u)
+      for (uint32_t i : byu[(size_t)ww * S + u]) idx.push_back(i), seg.push_back(2 * ww * S + u - 1);
+  }
   // level 0 + pairwise levels
   std::vector<uint32_t> cur_seg = seg;
   int C = 8;
@@ -192,18 +199,19 @@ void WeightedReducer<G>::plan(const std::vector<uint32_t> &w) {
     if (cur_seg.empty()) break;
   }
   // dense scatter: slot -> its single partial (or empty), via a permutation
-  std::vector<uint32_t> dst(2 * S + 1, 0), perm;
-  std::vector<int> at(2 * S, -1);
+  const size_t NS = (size_t)2 * nwin * S;
+  std::vector<uint32_t> dst(NS + 1, 0), perm;
+  std::vector<int> at(NS, -1);
   for (size_t k = 0; k < cur_seg.size(); ++k) at[cur_seg[k]] = (int)k;
-  for (uint32_t sl = 0; sl < 2 * S; ++sl) {
+  for (size_t sl = 0; sl < NS; ++sl) {
     dst[sl] = (uint32_t)perm.size();
     if (at[sl] >= 0) perm.push_back((uint32_t)at[sl]);
   }
-  dst[2 * S] = (uint32_t)perm.size();
+  dst[NS] = (uint32_t)perm.size();
   starts_.emplace_back();
   starts_.back().ensure(dst.size() * 4);
   MSM_HIP_CHECK(hipMemcpy(starts_.back().p, dst.data(), dst.size() * 4, hipMemcpyHostToDevice));
-  nout_.push_back(2 * S);
+  nout_.push_back(NS);
   std::vector<uint32_t> all = idx;  // [level-0 item list | final permutation]
   all.insert(all.end(), perm.begin(), perm.end());
   idx_.ensure(std::max<size_t>(all.size(), 1) * 4);
@@ -213,7 +221,7 @@ void WeightedReducer<G>::plan(const std::vector<uint32_t> &w) {
   for (size_t l = 0; l + 1 < nout_.size(); ++l) maxp = std::max(maxp, nout_[l]);
   part_[0].ensure(maxp * sizeof(Xyzz<F>));
   part_[1].ensure(maxp * sizeof(Xyzz<F>));
-  dense_buf_.ensure((size_t)2 * S * sizeof(Xyzz<F>));
+  dense_buf_.ensure(NS * sizeof(Xyzz<F>));
 }
 
 template <int G>
@@ -232,14 +240,15 @@ void WeightedReducer<G>::launch(hipStream_t s, const void *Sbuf) {
     MSM_HIP_CHECK(hipGetLastError());
     src = dst;
   }
-  dense_.launch(s, dense_buf_.p, 2, 1 << sbits_);
+  dense_.launch(s, dense_buf_.p, 2 * nwin_, 1 << sbits_);
 }
 
 template <int G>
-hfp::Jac<typename HostField<G>::F> WeightedReducer<G>::read(hipStream_t s) {
-  std::vector<hfp::Jac<HF>> T;
-  dense_.read(s, 2, T);
-  return horner(T, sbits_);
+std::vector<hfp::Jac<typename HostField<G>::F>> WeightedReducer<G>::read_windows(hipStream_t s) {
+  std::vector<hfp::Jac<HF>> T, out(nwin_);
+  dense_.read(s, 2 * nwin_, T);
+  for (int ww = 0; ww < nwin_; ++ww) out[ww] = horner(std::vector<hfp::Jac<HF>>{T[2 * ww], T[2 * ww + 1]}, sbits_);
+  return out;
 }
 
 template class WeightedReducer<MSM_GROUP>;
@@ -248,7 +257,7 @@ template class WeightedReducer<MSM_GROUP>;
 template <int G>
 Ches<G>::Ches(int device, const ChesParams &p) : dev_(device), p_(p) {
   DeviceGuard g(dev_);
-  if (p.q_exp < 2 || p.q_exp > 24 || p.h < 1 || p.h > 64 || (long)p.q_exp * p.h < 255)
+  if (p.q_exp < 2 || p.q_exp > 24 || p.h < 1 || p.h > 32 || (long)p.q_exp * p.h < 255)
     throw std::runtime_error("bad CHES parameters");
   const int q = 1 << p.q_exp;
   B_ = ches_bucket_set(q, p.a_h);
@@ -381,9 +390,20 @@ void Ches<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, hfp::J
   buckets_.ensure(NB * sizeof(Xyzz<F>));
 
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[0], s));
-  hipLaunchKernelGGL(k_ches_digits, dim3(nblk(n, 256)), dim3(256), 0, s, d_scalars, stride, n, p_.q_exp, p_.h,
-                     hash_.as<uint32_t>(), keys_.as<uint32_t>(), vals_.as<uint32_t>(), (uint32_t)B_.size(),
-                     (uint32_t)small_, (uint32_t)copies_);
+#define MSM_CHES_DIGITS(HT)                                                                                   \
+  hipLaunchKernelGGL(k_ches_digits<HT>, dim3(nblk(n, 256)), dim3(256), 0, s, d_scalars, stride, n, p_.q_exp, p_.h, \
+                     hash_.as<uint32_t>(), keys_.as<uint32_t>(), vals_.as<uint32_t>(), (uint32_t)B_.size(),      \
+                     (uint32_t)small_, (uint32_t)copies_)
+  switch (p_.h) {  // the h of the reference configurations (ches_config_files)
+    case 12: MSM_CHES_DIGITS(12); break;
+    case 13: MSM_CHES_DIGITS(13); break;
+    case 14: MSM_CHES_DIGITS(14); break;
+    case 16: MSM_CHES_DIGITS(16); break;
+    case 19: MSM_CHES_DIGITS(19); break;
+    case 20: MSM_CHES_DIGITS(20); break;
+    default: MSM_CHES_DIGITS(0); break;
+  }
+#undef MSM_CHES_DIGITS
   MSM_HIP_CHECK(hipGetLastError());
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[1], s));
   sort_.run(s, keys_.as<uint32_t>(), vals_.as<uint32_t>(), ne, (uint32_t)NB, sorted_.as<uint32_t>(),

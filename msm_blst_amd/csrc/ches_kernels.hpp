@@ -186,10 +186,15 @@ __device__ __forceinline__ void sub_r_if_ge(uint32_t s[8]) {
 // equal to sum s_i P_i for points of order r).
 // Top-digit entries whose bucket index k is <= small go to copy i % copies of
 // bucket k (copy 0 = k itself, copy c >= 1 = nb0 + (c-1) small + k - 1).
+// HT = compile-time digit count (fully unrolled: every hash lookup, H[d] and
+// H[d + 1] for both carry states, is issued before the carry chain resolves);
+// HT = 0 handles any h with a runtime loop.
+template <int HT>
 static __global__ void __launch_bounds__(256)
-    k_ches_digits(const uint8_t *__restrict__ scalars, size_t stride, size_t n, int q_exp, int h,
+    k_ches_digits(const uint8_t *__restrict__ scalars, size_t stride, size_t n, int q_exp, int h_rt,
                   const uint32_t *__restrict__ hash, uint32_t *__restrict__ keys, uint32_t *__restrict__ vals,
                   uint32_t nb0, uint32_t small, uint32_t copies) {
+  const int h = HT ? HT : h_rt;
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint8_t *sp = scalars + i * stride;
@@ -208,15 +213,15 @@ static __global__ void __launch_bounds__(256)
   sub_r_if_ge(s);
   s[8] = s[9] = 0;
   const uint32_t qmask = (1u << q_exp) - 1u;
-  uint32_t carry = 0;
-  for (int j = 0; j < h; ++j) {
+  auto digit = [&](int j) -> uint32_t {
     int off = j * q_exp;
     int wi = off >> 5, sh = off & 31;
     uint32_t lo = wi < 10 ? s[wi] : 0u, hi = wi + 1 < 10 ? s[wi + 1] : 0u;
-    uint32_t d = (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) & qmask;
-    uint32_t e = hash[d + carry];
-    carry = e >> 31;
-    size_t k = i * (size_t)h + j;
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) & qmask;
+  };
+  auto emit = [&](int j, uint32_t e) {
+    const size_t slot = i * (size_t)h + j;  // (i, j) of the table index 3(i h + j) + m - 1
+    const size_t k = (size_t)j * n + i;     // entry position: digit-major, coalesced stores
     uint32_t b = e & CH_IDX_MASK;
     if (j == h - 1 && b != 0 && b <= small) {
       uint32_t c = (uint32_t)(i % copies);
@@ -224,9 +229,32 @@ static __global__ void __launch_bounds__(256)
     }
     if (b) {
       keys[k] = b;
-      vals[k] = (uint32_t)(3 * k + ((e >> 24) & 3u)) | (e & 0x80000000u);
+      vals[k] = (uint32_t)(3 * slot + ((e >> 24) & 3u)) | (e & 0x80000000u);
     } else {
       keys[k] = KEY_NONE;
+    }
+  };
+  if constexpr (HT > 0) {
+    uint32_t e0[HT], e1[HT];
+#pragma unroll
+    for (int j = 0; j < HT; ++j) {
+      uint32_t d = digit(j);
+      e0[j] = hash[d];
+      e1[j] = hash[d + 1];
+    }
+    uint32_t carry = 0;
+#pragma unroll
+    for (int j = 0; j < HT; ++j) {
+      uint32_t e = carry ? e1[j] : e0[j];
+      carry = e >> 31;
+      emit(j, e);
+    }
+  } else {
+    uint32_t carry = 0;
+    for (int j = 0; j < h; ++j) {
+      uint32_t e = hash[digit(j) + carry];
+      carry = e >> 31;
+      emit(j, e);
     }
   }
 }

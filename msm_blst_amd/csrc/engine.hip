@@ -20,7 +20,10 @@ namespace msm {
 #if MSM_GROUP == 1  // group-independent: compiled once
 void BucketSort::run(hipStream_t s, const uint32_t *keys, const uint32_t *vals, size_t ne, uint32_t nb,
                      uint32_t *sorted, uint32_t *counts, uint32_t *offsets, uint32_t *order) {
-  const int ncb = (int)((nb + (1u << BS_FB_BITS) - 1) >> BS_FB_BITS);
+  // ~256 coarse bins (see bucket_sort.hpp), fine buckets per bin in [2^8, 2^12]
+  int fb_bits = 8;
+  while (fb_bits < BS_MAX_FB_BITS && ((size_t)nb >> fb_bits) > 384) ++fb_bits;
+  const int ncb = (int)(((size_t)nb + (1u << fb_bits) - 1) >> fb_bits);
   if (ncb > BS_MAX_CB) throw std::runtime_error("BucketSort: too many buckets");
   if (ne >= (1ull << 32)) throw std::runtime_error("BucketSort: too many entries");
   const int ntiles = (int)std::max<size_t>(1, (ne + BS_TILE - 1) / BS_TILE);
@@ -30,30 +33,27 @@ void BucketSort::run(hipStream_t s, const uint32_t *keys, const uint32_t *vals, 
   okeys.ensure(std::max<size_t>(ne, 1) * 4);
   ovals.ensure(std::max<size_t>(ne, 1) * 4);
   total.ensure(16);
-  sched.ensure((size_t)nb * 4);
-  iota.ensure((size_t)nb * 4);
-  size_t scan_tmp = 0, sort_tmp = 0;
+  size_t scan_tmp = 0;
   hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, ghist.as<uint32_t>(), gbase.as<uint32_t>(), (int)nslots, s);
-  hipcub::DeviceRadixSort::SortPairsDescending(nullptr, sort_tmp, sched.as<uint32_t>(), sched.as<uint32_t>(),
-                                               iota.as<uint32_t>(), order, (int)nb, 0, 8, s);
-  tmp.ensure(std::max(scan_tmp, sort_tmp) + (size_t)nb * 4);
-  uint32_t *sched_sorted = reinterpret_cast<uint32_t *>(tmp.as<uint8_t>() + std::max(scan_tmp, sort_tmp));
-  hipLaunchKernelGGL(k_bs_hist, dim3(ntiles), dim3(256), 0, s, keys, ne, ncb, ntiles, ghist.as<uint32_t>());
+  tmp.ensure(scan_tmp);
+  hipLaunchKernelGGL(k_bs_hist, dim3(ntiles), dim3(256), 0, s, keys, ne, fb_bits, ncb, ntiles, ghist.as<uint32_t>());
   MSM_HIP_CHECK(hipGetLastError());
   size_t tb = scan_tmp;
   MSM_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, ghist.as<uint32_t>(), gbase.as<uint32_t>(), (int)nslots, s));
   hipLaunchKernelGGL(k_bs_total, dim3(1), dim3(64), 0, s, gbase.as<uint32_t>(), ghist.as<uint32_t>(), nslots,
                      total.as<uint32_t>());
-  hipLaunchKernelGGL(k_bs_coarse, dim3(ntiles), dim3(256), 0, s, keys, vals, ne, ncb, ntiles, gbase.as<uint32_t>(),
-                     okeys.as<uint32_t>(), ovals.as<uint32_t>());
+  hipLaunchKernelGGL(k_bs_coarse, dim3(ntiles), dim3(256), 0, s, keys, vals, ne, fb_bits, ncb, ntiles,
+                     gbase.as<uint32_t>(), okeys.as<uint32_t>(), ovals.as<uint32_t>());
   MSM_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(k_bs_fine, dim3(ncb), dim3(512), 0, s, okeys.as<uint32_t>(), ovals.as<uint32_t>(), ncb, ntiles,
-                     gbase.as<uint32_t>(), total.as<uint32_t>(), nb, sorted, counts, offsets, sched.as<uint32_t>());
+  hipLaunchKernelGGL(k_bs_fine, dim3(ncb), dim3(1024), 0, s, okeys.as<uint32_t>(), ovals.as<uint32_t>(), fb_bits, ncb,
+                     ntiles, gbase.as<uint32_t>(), total.as<uint32_t>(), nb, sorted, counts, offsets);
   MSM_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(k_iota, dim3(nblk(nb, 256)), dim3(256), 0, s, iota.as<uint32_t>(), (size_t)nb);
-  tb = sort_tmp;
-  MSM_HIP_CHECK(hipcub::DeviceRadixSort::SortPairsDescending(tmp.p, tb, sched.as<uint32_t>(), sched_sorted,
-                                                             iota.as<uint32_t>(), order, (int)nb, 0, 8, s));
+  classes.ensure(256 * 4);
+  MSM_HIP_CHECK(hipMemsetAsync(classes.p, 0, 256 * 4, s));
+  hipLaunchKernelGGL(k_sched_hist, dim3(nblk(nb, 256)), dim3(256), 0, s, counts, nb, classes.as<uint32_t>());
+  hipLaunchKernelGGL(k_sched_scan, dim3(1), dim3(64), 0, s, classes.as<uint32_t>());
+  hipLaunchKernelGGL(k_sched_scatter, dim3(nblk(nb, 256)), dim3(256), 0, s, counts, nb, classes.as<uint32_t>(), order);
+  MSM_HIP_CHECK(hipGetLastError());
 }
 #endif
 
@@ -151,10 +151,15 @@ void Pippenger<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, i
                      buckets_.as<Xyzz<F>>(), NT);
   MSM_HIP_CHECK(hipGetLastError());
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[3], s));
-  std::vector<hfp::Jac<HF>> T;
-  dense_.launch(s, buckets_.p, W, (int)NB);
+  if (red_W_ != W) {  // bucket (w, b-1) has weight b in window w; plan once per window layout
+    std::vector<uint32_t> wt(NT), win(NT);
+    for (size_t k = 0; k < NT; ++k) wt[k] = (uint32_t)(k % NB) + 1, win[k] = (uint32_t)(k / NB);
+    red_.plan(wt, win, W);
+    red_W_ = W;
+  }
+  red_.launch(s, buckets_.p);
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[4], s));
-  dense_.read(s, W, T);
+  std::vector<hfp::Jac<HF>> T = red_.read_windows(s);
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[5], s));
   MSM_HIP_CHECK(hipStreamSynchronize(s));
   *out = horner(T, c);

@@ -65,9 +65,9 @@ struct HostField<2> {
 
 // Two-level LDS counting sort of (bucket, payload) entries (bucket_sort.hpp).
 // Produces payloads grouped by bucket, per-bucket counts/offsets and the
-// accumulation schedule: bucket ids ordered by count, descending (8-bit key).
+// accumulation schedule (bucket ids by descending count).
 struct BucketSort {
-  DevBuf ghist, gbase, okeys, ovals, total, sched, iota, tmp;
+  DevBuf ghist, gbase, okeys, ovals, total, classes, tmp;
   // keys[ne] (bucket < nb or 0xffffffff), vals[ne]; outputs sized ne / nb
   void run(hipStream_t s, const uint32_t *keys, const uint32_t *vals, size_t ne, uint32_t nb, uint32_t *sorted,
            uint32_t *counts, uint32_t *offsets, uint32_t *order);
@@ -96,33 +96,6 @@ hfp::Jac<HF> horner(const std::vector<hfp::Jac<HF>> &T, int c) {
   return ret;
 }
 
-// Plain Pippenger bucket method (ref src/multi_scalar.c:549-576) on one GPU.
-template <int G>
-class Pippenger {
- public:
-  typedef typename HostField<G>::F HF;
-  Pippenger(int device, int window_bits);
-  ~Pippenger();
-  // points in blst affine layout (Montgomery R=2^384); host or device memory
-  void set_points(const void *points_blst, size_t n, bool on_device, hipStream_t s);
-  // scalars: n little-endian byte strings with the given stride, on device
-  void run(hipStream_t s, const uint8_t *d_scalars, size_t stride, int nbits, hfp::Jac<HF> *out);
-  size_t npoints() const { return n_; }
-  void set_profiling(bool on) { profile_ = on; }
-  const PhaseTimes &times() const { return times_; }
-  int device() const { return dev_; }
-  int window_bits() const { return c_; }
-
- private:
-  int dev_, c_;
-  size_t n_ = 0;
-  bool profile_ = false;
-  PhaseTimes times_;
-  DevBuf pts_, keys_, vals_, counts_, offsets_, sorted_, order_, buckets_, tmp_;
-  BucketSort sort_;
-  DenseReducer<G> dense_;
-  std::vector<hipEvent_t> ev_;
-};
 
 // ---------------------------------------------------------------------------
 // CHES "nh + q/5" bucket-set method (ches.hip)
@@ -163,18 +136,50 @@ template <int G>
 class WeightedReducer {
  public:
   typedef typename HostField<G>::F HF;
-  void plan(const std::vector<uint32_t> &w);
+  // win[i] in [0, nwin): the window of bucket i (empty = all in window 0)
+  void plan(const std::vector<uint32_t> &w, const std::vector<uint32_t> &win, int nwin);
+  void plan(const std::vector<uint32_t> &w) { plan(w, {}, 1); }
   void launch(hipStream_t s, const void *S);   // device xyzz[w.size()]
-  hfp::Jac<HF> read(hipStream_t s);             // waits
+  std::vector<hfp::Jac<HF>> read_windows(hipStream_t s);  // per-window sums, waits
+  hfp::Jac<HF> read(hipStream_t s) { return read_windows(s)[0]; }
   size_t size() const { return bsize_; }
 
  private:
   size_t bsize_ = 0, final_perm_off_ = 0;
-  int sbits_ = 1;
+  int sbits_ = 1, nwin_ = 1;
   DevBuf idx_, dense_buf_, part_[2];
   std::vector<DevBuf> starts_;
   std::vector<size_t> nout_;
   ScanReducer<G> dense_;
+};
+
+// Plain Pippenger bucket method (ref src/multi_scalar.c:549-576) on one GPU.
+template <int G>
+class Pippenger {
+ public:
+  typedef typename HostField<G>::F HF;
+  Pippenger(int device, int window_bits);
+  ~Pippenger();
+  // points in blst affine layout (Montgomery R=2^384); host or device memory
+  void set_points(const void *points_blst, size_t n, bool on_device, hipStream_t s);
+  // scalars: n little-endian byte strings with the given stride, on device
+  void run(hipStream_t s, const uint8_t *d_scalars, size_t stride, int nbits, hfp::Jac<HF> *out);
+  size_t npoints() const { return n_; }
+  void set_profiling(bool on) { profile_ = on; }
+  const PhaseTimes &times() const { return times_; }
+  int device() const { return dev_; }
+  int window_bits() const { return c_; }
+
+ private:
+  int dev_, c_;
+  size_t n_ = 0;
+  bool profile_ = false;
+  PhaseTimes times_;
+  DevBuf pts_, keys_, vals_, counts_, offsets_, sorted_, order_, buckets_, tmp_;
+  BucketSort sort_;
+  WeightedReducer<G> red_;
+  int red_W_ = 0;  // window count the reducer plan was built for
+  std::vector<hipEvent_t> ev_;
 };
 
 template <int G>

@@ -197,9 +197,12 @@ static __global__ void k_iota(uint32_t *a, size_t n) {
   if (i < n) a[i] = (uint32_t)i;
 }
 
-// one lane per bucket, buckets visited in descending-size order
+// One lane per bucket, buckets visited in the schedule `order` (descending
+// entry count, BucketSort) so the 64 lanes of a wave run loops of nearly equal
+// length and the longest buckets start first.
 template <int G>
-__global__ void __launch_bounds__(256) k_accumulate(const uint32_t *__restrict__ order, const uint32_t *__restrict__ counts,
+__global__ void __launch_bounds__(256) k_accumulate(const uint32_t *__restrict__ order,
+                                                    const uint32_t *__restrict__ counts,
                                                     const uint32_t *__restrict__ offsets,
                                                     const uint32_t *__restrict__ sorted,
                                                     const Aff<typename FieldOf<G>::F> *__restrict__ pts,
