@@ -317,7 +317,7 @@ void Ches<G>::build_table(const void *pts, size_t n, bool on_device, hipStream_t
   hipLaunchKernelGGL(k_convert_points<G>, dim3(nblk(n, 256)), dim3(256), 0, s, (const uint64_t *)src,
                      base.as<Aff<F>>(), n);
   MSM_HIP_CHECK(hipGetLastError());
-  table_.ensure(K * n * sizeof(Aff<F>));
+  table_.ensure(K * n * sizeof(AffP<F>));
   const size_t chunk = std::min<size_t>(n, (size_t)1 << 16);
   DevBuf scratch, pref;
   scratch.ensure(K * chunk * sizeof(Xyzz<F>));
@@ -325,7 +325,7 @@ void Ches<G>::build_table(const void *pts, size_t n, bool on_device, hipStream_t
   for (size_t i0 = 0; i0 < n; i0 += chunk) {
     size_t cnt = std::min(chunk, n - i0);
     hipLaunchKernelGGL(k_ches_table<G>, dim3(nblk(cnt, 64)), dim3(64), 0, s, base.as<Aff<F>>(), i0, cnt, p_.q_exp,
-                       p_.h, scratch.as<Xyzz<F>>(), pref.as<F>(), table_.as<Aff<F>>());
+                       p_.h, scratch.as<Xyzz<F>>(), pref.as<F>(), table_.as<AffP<F>>());
     MSM_HIP_CHECK(hipGetLastError());
   }
   MSM_HIP_CHECK(hipStreamSynchronize(s));
@@ -346,10 +346,10 @@ void Ches<G>::set_table(const void *tab, size_t n, bool on_device, hipStream_t s
     MSM_HIP_CHECK(hipMemcpyAsync(stage.p, tab, cnt * 96 * G, hipMemcpyHostToDevice, s));
     src = stage.p;
   }
-  table_.ensure(std::max<size_t>(cnt, 1) * sizeof(Aff<F>));
+  table_.ensure(std::max<size_t>(cnt, 1) * sizeof(AffP<F>));
   if (cnt)
-    hipLaunchKernelGGL(k_convert_points<G>, dim3(nblk(cnt, 256)), dim3(256), 0, s, (const uint64_t *)src,
-                       table_.as<Aff<F>>(), cnt);
+    hipLaunchKernelGGL((k_convert_points<G, AffP<F>>), dim3(nblk(cnt, 256)), dim3(256), 0, s, (const uint64_t *)src,
+                       table_.as<AffP<F>>(), cnt);
   MSM_HIP_CHECK(hipGetLastError());
   MSM_HIP_CHECK(hipStreamSynchronize(s));
   n_ = n;
@@ -364,8 +364,8 @@ void Ches<G>::get_table(void *out, size_t first, size_t count, hipStream_t s) {
   if (!count) return;
   DevBuf o;
   o.ensure(count * 96 * G);
-  hipLaunchKernelGGL(k_export_affine<G>, dim3(nblk(count, 256)), dim3(256), 0, s, table_.as<Aff<F>>() + first,
-                     o.as<uint64_t>(), count);
+  hipLaunchKernelGGL((k_export_affine<G, AffP<F>>), dim3(nblk(count, 256)), dim3(256), 0, s,
+                     table_.as<AffP<F>>() + first, o.as<uint64_t>(), count);
   MSM_HIP_CHECK(hipGetLastError());
   MSM_HIP_CHECK(hipMemcpyAsync(out, o.p, count * 96 * G, hipMemcpyDeviceToHost, s));
   MSM_HIP_CHECK(hipStreamSynchronize(s));
@@ -409,8 +409,8 @@ void Ches<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, hfp::J
   sort_.run(s, keys_.as<uint32_t>(), vals_.as<uint32_t>(), ne, (uint32_t)NB, sorted_.as<uint32_t>(),
             counts_.as<uint32_t>(), offsets_.as<uint32_t>(), order_.as<uint32_t>());
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[2], s));
-  hipLaunchKernelGGL(k_accumulate<G>, dim3(nblk(NB, 256)), dim3(256), 0, s, order_.as<uint32_t>(),
-                     counts_.as<uint32_t>(), offsets_.as<uint32_t>(), sorted_.as<uint32_t>(), table_.as<Aff<F>>(),
+  hipLaunchKernelGGL((k_accumulate<G, AffP<F>>), dim3(nblk(NB, 256)), dim3(256), 0, s, order_.as<uint32_t>(),
+                     counts_.as<uint32_t>(), offsets_.as<uint32_t>(), sorted_.as<uint32_t>(), table_.as<AffP<F>>(),
                      buckets_.as<Xyzz<F>>(), NB);
   MSM_HIP_CHECK(hipGetLastError());
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[3], s));

@@ -77,19 +77,19 @@ template <int G>
 static __global__ void __launch_bounds__(256)
     k_ches_table(const Aff<typename FieldOf<G>::F> *__restrict__ P, size_t i0, size_t cnt, int q_exp, int h,
                  Xyzz<typename FieldOf<G>::F> *__restrict__ scratch, typename FieldOf<G>::F *__restrict__ pref,
-                 Aff<typename FieldOf<G>::F> *__restrict__ T) {
+                 AffP<typename FieldOf<G>::F> *__restrict__ T) {
   typedef typename FieldOf<G>::F F;
   size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= cnt) return;
   const size_t i = i0 + t;
   const int K = 3 * h;
   Aff<F> p = ld16(&P[i]);
-  Aff<F> *out = T + (size_t)K * i;
+  AffP<F> *out = T + (size_t)K * i;
   if (f_is_zero_exact(p.x) && f_is_zero_exact(p.y)) {  // infinity: every multiple is infinity
     Aff<F> z;
     f_zero(z.x);
     f_zero(z.y);
-    for (int k = 0; k < K; ++k) st16(&out[k], z);
+    for (int k = 0; k < K; ++k) st_point(&out[k], z);
     return;
   }
   Xyzz<F> Q;
@@ -140,18 +140,17 @@ static __global__ void __launch_bounds__(256)
     f_mul(r.y, a.y, izzz);
     f_csub(r.x);
     f_csub(r.y);
-    st16(&out[k], r);
+    st_point(&out[k], r);
   }
 }
 
 // internal affine -> blst affine (canonical Montgomery, R = 2^384)
-template <int G>
-__global__ void k_export_affine(const Aff<typename FieldOf<G>::F> *__restrict__ in, uint64_t *__restrict__ out,
-                                size_t n) {
+template <int G, class PT>
+__global__ void k_export_affine(const PT *__restrict__ in, uint64_t *__restrict__ out, size_t n) {
   typedef typename FieldOf<G>::F F;
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  Aff<F> a = ld16(&in[i]);
+  Aff<F> a = ld_point(&in[i]);
   uint64_t *o = out + i * 12 * G;
   if (f_is_zero_exact(a.x) && f_is_zero_exact(a.y)) {
     for (int k = 0; k < 12 * G; ++k) o[k] = 0;

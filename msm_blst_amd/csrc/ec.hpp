@@ -74,10 +74,7 @@ __device__ __forceinline__ void xyzz_dbl(Xyzz<F> &r, const Xyzz<F> &a) {
   f_sub4(X3, X3, S);       // < 10p
   f_nred(X3);              // S
   f_sub4(t, S, X3);        // < 6p
-  f_mul(t, t, M);          // S
-  f_mul(Y3, W, a.y);       // S
-  f_sub4(Y3, t, Y3);       // < 6p
-  f_nred(Y3);              // S
+  f_mul_sub(Y3, t, M, W, a.y);  // M (S - X3) - W Y   S (one reduction)
   f_mul(r.zz, V, a.zz);
   f_mul(r.zzz, W, a.zzz);
   r.x = X3;
@@ -127,10 +124,7 @@ __device__ __forceinline__ void xyzz_madd(Xyzz<F> &acc, const Aff<F> &p, bool ne
   f_sub4(X3, X3, Q);       // < 14p
   f_nred(X3);              // X3 = R^2 - PPP - 2Q  S
   f_sub4(t, Q, X3);        // < 6p
-  f_mul(t, t, R);          // R (Q - X3)           S
-  f_mul(Y3, acc.y, PPP);   // Y1 PPP               S
-  f_sub4(Y3, t, Y3);       // < 6p
-  f_nred(Y3);              // S
+  f_mul_sub(Y3, t, R, acc.y, PPP);  // R (Q - X3) - Y1 PPP   S (one reduction)
   f_mul(acc.zz, acc.zz, PP);
   f_mul(acc.zzz, acc.zzz, PPP);
   acc.x = X3;
@@ -175,10 +169,7 @@ __device__ __forceinline__ void xyzz_add(Xyzz<F> &acc, const Xyzz<F> &b) {
   f_sub4(X3, X3, Q);
   f_nred(X3);
   f_sub4(t, Q, X3);
-  f_mul(t, t, R);
-  f_mul(Y3, S1, PPP);
-  f_sub4(Y3, t, Y3);
-  f_nred(Y3);
+  f_mul_sub(Y3, t, R, S1, PPP);  // R (Q - X3) - S1 PPP   S (one reduction)
   f_mul(acc.zz, acc.zz, b.zz);
   f_mul(acc.zz, acc.zz, PP);
   f_mul(acc.zzz, acc.zzz, b.zzz);

@@ -50,6 +50,31 @@ __device__ __forceinline__ void st16(T *p, const T &v) {
   for (int i = 0; i < (int)(sizeof(T) / 16); ++i) d[i] = tmp[i];
 }
 
+// Affine point padded to a multiple of 128 B: one row of the CHES table per
+// 128-B cache line (G1: 112 -> 128 B, G2: 224 -> 256 B), so a random gather
+// touches the minimum number of lines.
+template <class F>
+struct AffP {
+  F x, y;
+  uint32_t pad[((128 - (2 * sizeof(F)) % 128) % 128) / 4];
+};
+template <class F>
+__device__ __forceinline__ Aff<F> ld_point(const Aff<F> *p) {
+  return ld16(p);
+}
+template <class F>
+__device__ __forceinline__ Aff<F> ld_point(const AffP<F> *p) {
+  return ld16(reinterpret_cast<const Aff<F> *>(p));
+}
+template <class F>
+__device__ __forceinline__ void st_point(Aff<F> *p, const Aff<F> &a) {
+  st16(p, a);
+}
+template <class F>
+__device__ __forceinline__ void st_point(AffP<F> *p, const Aff<F> &a) {
+  st16(reinterpret_cast<Aff<F> *>(p), a);
+}
+
 // ---- blst 6x64 LE  <->  14 x 28-bit limbs ----
 __device__ __forceinline__ void unpack384(Fp &r, const uint64_t *l) {
   uint32_t w[12];
@@ -111,9 +136,8 @@ __device__ __forceinline__ void f_to_blst(uint64_t *l, const Fp2 &a) {
 // ---------------------------------------------------------------------------
 // point conversion: blst affine (Montgomery R=2^384) -> internal affine limbs
 // ---------------------------------------------------------------------------
-template <int G>
-__global__ void k_convert_points(const uint64_t *__restrict__ in, Aff<typename FieldOf<G>::F> *__restrict__ out,
-                                 size_t n) {
+template <int G, class PT = Aff<typename FieldOf<G>::F>>
+__global__ void k_convert_points(const uint64_t *__restrict__ in, PT *__restrict__ out, size_t n) {
   typedef typename FieldOf<G>::F F;
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -121,7 +145,7 @@ __global__ void k_convert_points(const uint64_t *__restrict__ in, Aff<typename F
   Aff<F> a;
   f_from_blst(a.x, p);
   f_from_blst(a.y, p + 6 * G);
-  st16(&out[i], a);
+  st_point(&out[i], a);
 }
 
 // ---------------------------------------------------------------------------
@@ -200,12 +224,12 @@ static __global__ void k_iota(uint32_t *a, size_t n) {
 // One lane per bucket, buckets visited in the schedule `order` (descending
 // entry count, BucketSort) so the 64 lanes of a wave run loops of nearly equal
 // length and the longest buckets start first.
-template <int G>
+template <int G, class PT = Aff<typename FieldOf<G>::F>>
 __global__ void __launch_bounds__(256) k_accumulate(const uint32_t *__restrict__ order,
                                                     const uint32_t *__restrict__ counts,
                                                     const uint32_t *__restrict__ offsets,
                                                     const uint32_t *__restrict__ sorted,
-                                                    const Aff<typename FieldOf<G>::F> *__restrict__ pts,
+                                                    const PT *__restrict__ pts,
                                                     Xyzz<typename FieldOf<G>::F> *__restrict__ buckets, size_t nbuckets) {
   typedef typename FieldOf<G>::F F;
   size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -216,7 +240,7 @@ __global__ void __launch_bounds__(256) k_accumulate(const uint32_t *__restrict__
   xyzz_set_inf(acc);
   for (uint32_t k = 0; k < cnt; ++k) {
     uint32_t e = sorted[off + k];
-    Aff<F> p = ld16(&pts[e & 0x7fffffffu]);
+    Aff<F> p = ld_point(&pts[e & 0x7fffffffu]);
     if (f_is_zero_exact(p.x) && f_is_zero_exact(p.y)) continue;  // affine infinity (ec_ops.h:717)
     xyzz_madd(acc, p, (e >> 31) != 0);
   }
