@@ -70,6 +70,37 @@ def timed_steps(step, ctx, steps, warmup, world, dev):
     return res, elapsed, acc_ms, tot_ms, ctx.phase_times()
 
 
+def timed_batch(ctx, steps, warmup, world, dev, add):
+    """CHES batch mode: the K steps are K MSMs issued as one pipelined batch
+    (msm_ches_ctx_mult_batch: MSM k's bucket-reduction tail overlaps MSM k+1);
+    for N > 1 each step's partial is then exchanged and folded.  Same bracketing
+    (barrier + synchronize, max over ranks) as timed_steps."""
+    import torch
+    from msm_blst_amd import dist as mdist
+    if warmup:
+        ctx._bench_batch(warmup)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize(dev)
+    ctx.set_profiling(True)
+    t_start = time.perf_counter()
+    parts = ctx._bench_batch(steps)
+    if world > 1:
+        res = [mdist.fold(mdist.gather_partials(p, 1, dev), add) for p in parts][-1]
+    else:
+        res = parts[-1]
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t_start
+    acc_ms = [ctx.phase_times()["accumulate"]]
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return res, elapsed, acc_ms
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -79,6 +110,8 @@ def main():
     ap.add_argument("--method", choices=("ches", "pippenger"), default="ches")
     ap.add_argument("--window", type=int, default=16, help="plain Pippenger window bits")
     ap.add_argument("--no-compare", action="store_true", help="skip timing the other method (N = 1)")
+    ap.add_argument("--no-batch", action="store_true",
+                    help="CHES: time K independent synchronous MSMs instead of one pipelined batch of K")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-log-n", type=int, default=20)
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
@@ -122,6 +155,11 @@ def main():
 
             def mult():
                 return ctx.mult(d_sc.data_ptr(), 32, on_device=True, stream=stream.cuda_stream)
+
+            def mult_batch(k):  # k MSMs on the same resident scalars, pipelined (set_stride 0)
+                return ctx.mult_batch(d_sc.data_ptr(), k, 32, set_stride=0, on_device=True,
+                                      stream=stream.cuda_stream)
+            ctx._bench_batch = mult_batch
         else:
             ctx = m.MSMContext(1, local, args.window)
             ctx.set_points(pts, n, stream=stream.cuda_stream)
@@ -140,12 +178,25 @@ def main():
         return ctx, step
 
     ctx, step = make(args.method)
-    res, elapsed, acc_ms, tot_ms, phases = timed_steps(step, ctx, args.steps, args.warmup, world, dev)
+    batched = args.method == "ches" and not args.no_batch
+    if batched:
+        res, elapsed, acc_ms = timed_batch(ctx, args.steps, args.warmup, world, dev, add)
+        ctx.mult(d_sc.data_ptr(), 32, on_device=True, stream=stream.cuda_stream)  # one profiled single MSM
+        phases = ctx.phase_times()
+    else:
+        res, elapsed, acc_ms, tot_ms, phases = timed_steps(step, ctx, args.steps, args.warmup, world, dev)
 
     gold = json.load(open(os.path.join(REPO, "tests", "golden", "msm_g1.json")))
     want = [c["compressed"] for c in gold["cases"] if c["n"] == n and c["seed"] == 1 and c["case"] == "rand"]
     parity = (m.compress(1, res).hex() == want[0]) if (world == 1 and want) else None
 
+    sync = None
+    if batched and world == 1 and not args.no_compare:  # the same MSMs issued one by one (no overlap)
+        sres, sel, _, _, sph = timed_steps(step, ctx, args.steps, 1, world, dev)
+        sync = {"value": round(n * args.steps / sel, 1), "unit": "pairs/s",
+                "ms_per_step": round(sel / args.steps * 1e3, 4),
+                "parity_vs_reference": (m.compress(1, sres).hex() == want[0]) if want else None,
+                "note": "K synchronous msm_ches_ctx_mult calls (per-MSM latency)"}
     other = None
     if world == 1 and not args.no_compare:
         ometh = "pippenger" if args.method == "ches" else "ches"
@@ -220,8 +271,12 @@ def main():
                           "work": f"{madds} xyzz madds x {FPMUL_PER_MADD} Fp-mul",
                           "peak_basis": "measured register-resident Fp-mul kernel (tools/microbench/fp_rate.hip)"},
         "phases_ms": {k: round(v, 4) for k, v in phases.items()},
+        "phases_note": "one synchronous MSM (profiled) after the timed region" if batched else "last timed step",
+        "pipelined_batch": batched,
         "parity_vs_reference": parity,
-        "methods": {args.method: {"value": round(value, 1), "ms_per_step": round(elapsed / args.steps * 1e3, 4)},
+        "methods": {args.method + ("_batch" if batched else ""): {"value": round(value, 1),
+                                                                   "ms_per_step": round(elapsed / args.steps * 1e3, 4)},
+                    **({"ches_sync": sync} if sync else {}),
                     **({other["method"]: other} if other else {})},
         "cpu_baseline": cpu,
     }

@@ -113,6 +113,14 @@ int msm_ches_ctx_get_table(msm_ches_ctx *ctx, void *out_affine, size_t first, si
 /* scalars: npoints 32-byte LE strings with the given stride (>= 32), host or device */
 int msm_ches_ctx_mult(msm_ches_ctx *ctx, void *ret, const byte *scalars, size_t stride, int scalars_on_device,
                       void *hip_stream);
+/* count MSMs over the same points: scalar set k (npoints strings of `stride` bytes)
+ * at scalars + k * set_stride; rets: count Jacobians.  Pipelined on the device:
+ * MSM k's latency-bound bucket-reduction tail runs on a second stream beside
+ * MSM k+1's digit conversion, sort and accumulation (the batched-MSM shape of a
+ * prover committing many polynomials to one SRS).  Results equal count calls
+ * of msm_ches_ctx_mult. */
+int msm_ches_ctx_mult_batch(msm_ches_ctx *ctx, void *rets, const byte *scalars, size_t stride, size_t set_stride,
+                            size_t count, int scalars_on_device, void *hip_stream);
 int msm_ches_ctx_set_profiling(msm_ches_ctx *ctx, int on);
 int msm_ches_ctx_phase_times(const msm_ches_ctx *ctx, float out[6]);
 size_t msm_ches_ctx_bucket_count(const msm_ches_ctx *ctx);

@@ -60,6 +60,7 @@ def lib():
     L.msm_ches_ctx_set_table.argtypes = [vp, vp, sz, i32, vp]
     L.msm_ches_ctx_get_table.argtypes = [vp, vp, sz, sz]
     L.msm_ches_ctx_mult.argtypes = [vp, vp, vp, sz, i32, vp]
+    L.msm_ches_ctx_mult_batch.argtypes = [vp, vp, vp, sz, sz, sz, i32, vp]
     L.msm_ches_ctx_set_profiling.argtypes = [vp, i32]
     L.msm_ches_ctx_phase_times.argtypes = [vp, vp]
     L.msm_ches_ctx_bucket_count.argtypes = [vp]

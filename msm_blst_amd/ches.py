@@ -89,6 +89,20 @@ class CHESContext:
         check(lib().msm_ches_ctx_mult(self._ctx, ret, ptr, stride, int(bool(on_device)), stream))
         return bytes(ret)
 
+    def mult_batch(self, scalars, count, stride=32, set_stride=None, on_device=False, stream=None):
+        """`count` MSMs over the same points (scalar set k at k * set_stride bytes;
+        set_stride=0 repeats one set), pipelined on the device.  Returns a list of
+        Jacobian byte strings."""
+        if set_stride is None:
+            set_stride = self.n * stride
+        rets = (ctypes.c_uint8 * (JAC_BYTES[self.group] * count))()
+        ptr = scalars if on_device else _buf(scalars)
+        check(lib().msm_ches_ctx_mult_batch(self._ctx, rets, ptr, stride, set_stride, count, int(bool(on_device)),
+                                            stream))
+        raw = bytes(rets)
+        nb = JAC_BYTES[self.group]
+        return [raw[k * nb:(k + 1) * nb] for k in range(count)]
+
     def bucket_count(self):
         return lib().msm_ches_ctx_bucket_count(self._ctx)
 

@@ -400,6 +400,35 @@ int msm_ches_ctx_mult(msm_ches_ctx *ctx, void *ret, const byte *scalars, size_t 
   }
 }
 
+int msm_ches_ctx_mult_batch(msm_ches_ctx *ctx, void *rets, const byte *scalars, size_t stride, size_t set_stride,
+                            size_t count, int on_device, void *stream) {
+  if (!ctx || (!rets && count) || stride < 32) return fail(MSM_E_ARG, "bad args (stride must be >= 32)");
+  try {
+    DeviceGuard g(ctx->device);
+    hipStream_t s = (hipStream_t)stream;
+    size_t n = CHES_DISPATCH(ctx, npoints());
+    const uint8_t *d = scalars;
+    if (!on_device && n && count) {
+      size_t span = (count - 1) * set_stride + n * stride;
+      ctx->scalars.ensure(span + 16);
+      MSM_HIP_CHECK(hipMemcpyAsync(ctx->scalars.p, scalars, span, hipMemcpyHostToDevice, s));
+      d = ctx->scalars.as<uint8_t>();
+    }
+    if (ctx->group == 1) {
+      std::vector<hfp::Jac<hfp::Fp>> out(count);
+      ctx->g1->run_batch(s, d, stride, set_stride, count, out.data());
+      memcpy(rets, out.data(), count * sizeof(out[0]));
+    } else {
+      std::vector<hfp::Jac<hfp::Fp2>> out(count);
+      ctx->g2->run_batch(s, d, stride, set_stride, count, out.data());
+      memcpy(rets, out.data(), count * sizeof(out[0]));
+    }
+    return MSM_OK;
+  } catch (const std::exception &e) {
+    return fail(MSM_E_HIP, e.what());
+  }
+}
+
 int msm_ches_ctx_set_profiling(msm_ches_ctx *ctx, int on) {
   if (!ctx) return fail(MSM_E_ARG, "null ctx");
   CHES_DISPATCH(ctx, set_profiling(on != 0));

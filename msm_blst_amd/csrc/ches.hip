@@ -219,36 +219,63 @@ void WeightedReducer<G>::plan(const std::vector<uint32_t> &w, const std::vector<
   final_perm_off_ = idx.size();
   size_t maxp = 1;
   for (size_t l = 0; l + 1 < nout_.size(); ++l) maxp = std::max(maxp, nout_[l]);
-  part_[0].ensure(maxp * sizeof(Xyzz<F>));
-  part_[1].ensure(maxp * sizeof(Xyzz<F>));
-  dense_buf_.ensure(NS * sizeof(Xyzz<F>));
+  for (int st = 0; st < NSETS; ++st) {
+    part_[st][0].ensure(maxp * sizeof(Xyzz<F>));
+    part_[st][1].ensure(maxp * sizeof(Xyzz<F>));
+    dense_buf_[st].ensure(NS * sizeof(Xyzz<F>));
+  }
 }
 
 template <int G>
-void WeightedReducer<G>::launch(hipStream_t s, const void *Sbuf) {
+void WeightedReducer<G>::launch_head(hipStream_t s, const void *Sbuf, int set) {
   typedef typename FieldOf<G>::F F;
   const size_t L = nout_.size();
   const Xyzz<F> *src = reinterpret_cast<const Xyzz<F> *>(Sbuf);
-  const uint32_t *idx = idx_.as<uint32_t>();
-  for (size_t l = 0; l < L; ++l) {
+  Xyzz<F> *dst = L == 1 ? dense_buf_[set].as<Xyzz<F>>() : part_[set][0].as<Xyzz<F>>();
+  const uint32_t *ix = L == 1 ? idx_.as<uint32_t>() + final_perm_off_ : idx_.as<uint32_t>();
+  if (nout_[0])
+    hipLaunchKernelGGL(k_segsum<G>, dim3(nblk(nout_[0], 64)), dim3(64), 0, s, src, ix, starts_[0].as<uint32_t>(), dst,
+                       nout_[0]);
+  MSM_HIP_CHECK(hipGetLastError());
+}
+
+template <int G>
+void WeightedReducer<G>::launch_tail(hipStream_t s, int set) {
+  typedef typename FieldOf<G>::F F;
+  const size_t L = nout_.size();
+  const Xyzz<F> *src = part_[set][0].as<Xyzz<F>>();
+  for (size_t l = 1; l < L; ++l) {
     const bool last = l + 1 == L;
-    Xyzz<F> *dst = last ? dense_buf_.as<Xyzz<F>>() : part_[l & 1].as<Xyzz<F>>();
-    const uint32_t *ix = l == 0 ? idx : (last ? idx + final_perm_off_ : nullptr);
+    Xyzz<F> *dst = last ? dense_buf_[set].as<Xyzz<F>>() : part_[set][l & 1].as<Xyzz<F>>();
+    const uint32_t *ix = last ? idx_.as<uint32_t>() + final_perm_off_ : nullptr;
     if (nout_[l])
       hipLaunchKernelGGL(k_segsum<G>, dim3(nblk(nout_[l], 64)), dim3(64), 0, s, src, ix, starts_[l].as<uint32_t>(),
                          dst, nout_[l]);
     MSM_HIP_CHECK(hipGetLastError());
     src = dst;
   }
-  dense_.launch(s, dense_buf_.p, 2 * nwin_, 1 << sbits_);
+  dense_[set].launch(s, dense_buf_[set].p, 2 * nwin_, 1 << sbits_);
+}
+
+template <int G>
+void WeightedReducer<G>::copy_out(hipStream_t s, int set, void *host) {
+  MSM_HIP_CHECK(hipMemcpyAsync(host, dense_[set].fin.p, out_bytes(), hipMemcpyDeviceToHost, s));
+}
+
+template <int G>
+std::vector<hfp::Jac<typename HostField<G>::F>> WeightedReducer<G>::combine(const void *host) const {
+  const hfp::Jac<HF> *T = reinterpret_cast<const hfp::Jac<HF> *>(host);
+  std::vector<hfp::Jac<HF>> out(nwin_);
+  for (int ww = 0; ww < nwin_; ++ww) out[ww] = horner(std::vector<hfp::Jac<HF>>{T[2 * ww], T[2 * ww + 1]}, sbits_);
+  return out;
 }
 
 template <int G>
 std::vector<hfp::Jac<typename HostField<G>::F>> WeightedReducer<G>::read_windows(hipStream_t s) {
-  std::vector<hfp::Jac<HF>> T, out(nwin_);
-  dense_.read(s, 2 * nwin_, T);
-  for (int ww = 0; ww < nwin_; ++ww) out[ww] = horner(std::vector<hfp::Jac<HF>>{T[2 * ww], T[2 * ww + 1]}, sbits_);
-  return out;
+  std::vector<uint8_t> host(out_bytes());
+  copy_out(s, 0, host.data());
+  MSM_HIP_CHECK(hipStreamSynchronize(s));
+  return combine(host.data());
 }
 
 template class WeightedReducer<MSM_GROUP>;
@@ -275,6 +302,13 @@ Ches<G>::Ches(int device, const ChesParams &p) : dev_(device), p_(p) {
 template <int G>
 Ches<G>::~Ches() {
   for (auto &e : ev_) (void)hipEventDestroy(e);
+  for (auto &e : acc_ev_) (void)hipEventDestroy(e);
+  for (int k = 0; k < 2; ++k) {
+    if (ev_head_[k]) (void)hipEventDestroy(ev_head_[k]);
+    if (ev_tail_[k]) (void)hipEventDestroy(ev_tail_[k]);
+    if (host_out_[k]) (void)hipHostFree(host_out_[k]);
+  }
+  if (tail_) (void)hipStreamDestroy(tail_);
 }
 
 // bucket space = B plus (copies_ - 1) copies of the small buckets 1..small_;
@@ -372,14 +406,8 @@ void Ches<G>::get_table(void *out, size_t first, size_t count, hipStream_t s) {
 }
 
 template <int G>
-void Ches<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, hfp::Jac<HF> *out) {
+void Ches<G>::front(hipStream_t s, const uint8_t *d_scalars, size_t stride, hipEvent_t acc0, hipEvent_t acc1) {
   typedef typename FieldOf<G>::F F;
-  DeviceGuard g(dev_);
-  if (stride < 32) throw std::runtime_error("CHES scalars must be 32-byte strings");
-  if (n_ == 0) {
-    std::memset(out, 0, sizeof(*out));
-    return;
-  }
   const size_t n = n_, h = (size_t)p_.h, ne = n * h, NB = bucket_count();
   keys_.ensure(ne * 4);
   vals_.ensure(ne * 4);
@@ -388,7 +416,6 @@ void Ches<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, hfp::J
   offsets_.ensure(NB * 4);
   order_.ensure(NB * 4);
   buckets_.ensure(NB * sizeof(Xyzz<F>));
-
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[0], s));
 #define MSM_CHES_DIGITS(HT)                                                                                   \
   hipLaunchKernelGGL(k_ches_digits<HT>, dim3(nblk(n, 256)), dim3(256), 0, s, d_scalars, stride, n, p_.q_exp, p_.h, \
@@ -409,11 +436,24 @@ void Ches<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, hfp::J
   sort_.run(s, keys_.as<uint32_t>(), vals_.as<uint32_t>(), ne, (uint32_t)NB, sorted_.as<uint32_t>(),
             counts_.as<uint32_t>(), offsets_.as<uint32_t>(), order_.as<uint32_t>());
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[2], s));
+  if (acc0) MSM_HIP_CHECK(hipEventRecord(acc0, s));
   hipLaunchKernelGGL((k_accumulate<G, AffP<F>>), dim3(nblk(NB, 256)), dim3(256), 0, s, order_.as<uint32_t>(),
                      counts_.as<uint32_t>(), offsets_.as<uint32_t>(), sorted_.as<uint32_t>(), table_.as<AffP<F>>(),
                      buckets_.as<Xyzz<F>>(), NB);
   MSM_HIP_CHECK(hipGetLastError());
+  if (acc1) MSM_HIP_CHECK(hipEventRecord(acc1, s));
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[3], s));
+}
+
+template <int G>
+void Ches<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, hfp::Jac<HF> *out) {
+  DeviceGuard g(dev_);
+  if (stride < 32) throw std::runtime_error("CHES scalars must be 32-byte strings");
+  if (n_ == 0) {
+    std::memset(out, 0, sizeof(*out));
+    return;
+  }
+  front(s, d_scalars, stride);
   red_.launch(s, buckets_.p);
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[4], s));
   *out = red_.read(s);
@@ -434,6 +474,70 @@ void Ches<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, hfp::J
     MSM_HIP_CHECK(hipEventElapsedTime(&ms, ev_[0], ev_[5]));
     times_.total = ms;
     times_.accumulate_launches = 1;
+  }
+}
+
+template <int G>
+void Ches<G>::run_batch(hipStream_t s, const uint8_t *d_scalars, size_t stride, size_t set_stride, size_t count,
+                        hfp::Jac<HF> *outs) {
+  DeviceGuard g(dev_);
+  if (stride < 32) throw std::runtime_error("CHES scalars must be 32-byte strings");
+  if (count == 0) return;
+  if (n_ == 0) {
+    std::memset(outs, 0, sizeof(*outs) * count);
+    return;
+  }
+  if (!tail_) {
+    MSM_HIP_CHECK(hipStreamCreateWithFlags(&tail_, hipStreamNonBlocking));
+    for (int k = 0; k < 2; ++k) {
+      MSM_HIP_CHECK(hipEventCreateWithFlags(&ev_head_[k], hipEventDisableTiming));
+      MSM_HIP_CHECK(hipEventCreateWithFlags(&ev_tail_[k], hipEventDisableTiming));
+      MSM_HIP_CHECK(hipHostMalloc(&host_out_[k], red_.out_bytes() + 64, hipHostMallocDefault));
+    }
+  }
+  const bool prof = profile_;
+  profile_ = false;
+  if (prof)
+    while (acc_ev_.size() < 2 * count) {
+      hipEvent_t e;
+      MSM_HIP_CHECK(hipEventCreate(&e));
+      acc_ev_.push_back(e);
+    }
+  // MSM k: front + level 0 on s; tail on tail_ (buffer set k & 1), then the host
+  // combines MSM k - 1 while the GPU runs MSM k.
+  for (size_t k = 0; k <= count; ++k) {
+    if (k < count) {
+      const int set = (int)(k & 1);
+      front(s, d_scalars + k * set_stride, stride, prof ? acc_ev_[2 * k] : nullptr, prof ? acc_ev_[2 * k + 1] : nullptr);
+      if (k >= 2) MSM_HIP_CHECK(hipStreamWaitEvent(s, ev_tail_[set], 0));  // set's buffers free again
+      red_.launch_head(s, buckets_.p, set);
+      MSM_HIP_CHECK(hipEventRecord(ev_head_[set], s));
+      MSM_HIP_CHECK(hipStreamWaitEvent(tail_, ev_head_[set], 0));
+      red_.launch_tail(tail_, set);
+      red_.copy_out(tail_, set, host_out_[set]);
+      MSM_HIP_CHECK(hipEventRecord(ev_tail_[set], tail_));
+    }
+    if (k >= 1) {
+      const int pset = (int)((k - 1) & 1);
+      MSM_HIP_CHECK(hipEventSynchronize(ev_tail_[pset]));
+      outs[k - 1] = red_.combine(host_out_[pset])[0];
+    }
+  }
+  // the caller's stream observes completion of every tail
+  MSM_HIP_CHECK(hipEventRecord(ev_tail_[0], tail_));
+  MSM_HIP_CHECK(hipStreamWaitEvent(s, ev_tail_[0], 0));
+  profile_ = prof;
+  if (prof) {  // average accumulation time over the batch (HIP events on stream s)
+    float sum = 0;
+    for (size_t k = 0; k < count; ++k) {
+      float ms;
+      MSM_HIP_CHECK(hipEventSynchronize(acc_ev_[2 * k + 1]));
+      MSM_HIP_CHECK(hipEventElapsedTime(&ms, acc_ev_[2 * k], acc_ev_[2 * k + 1]));
+      sum += ms;
+    }
+    times_ = PhaseTimes();
+    times_.accumulate = sum / (float)count;
+    times_.accumulate_launches = (int)count;
   }
 }
 

@@ -120,37 +120,46 @@ template <int G>
 struct ScanReducer {
   typedef typename HostField<G>::F HF;
   DevBuf buf[2], fin;
+  // enqueue: fin <- W blst Jacobians (144 G bytes each)
   void launch(hipStream_t s, const void *A, int W, int S);
   void read(hipStream_t s, int W, std::vector<hfp::Jac<HF>> &out);
-
- private:
-  int last_ = 0;
 };
 
 // sum_i w[i] * S_i for arbitrary non-negative bucket weights w (w = 0: bucket
 // ignored) over device xyzz buckets S (replaces ref multi_scalar.c:301-321).
 // Two regroupings by the low and high halves of w[i] (2 xyzz adds per bucket),
 // then a dense 2-window ScanReducer and one 2^s Horner step on the host.  The
-// plan depends only on w and is built once.
+// plan depends only on w and is built once.  Two independent buffer sets let
+// the latency-bound tail of one MSM (launch_tail, on a second stream) overlap
+// the next MSM's digits/sort/accumulation/level-0 (launch_head).
 template <int G>
 class WeightedReducer {
  public:
   typedef typename HostField<G>::F HF;
+  static constexpr int NSETS = 2;
   // win[i] in [0, nwin): the window of bucket i (empty = all in window 0)
   void plan(const std::vector<uint32_t> &w, const std::vector<uint32_t> &win, int nwin);
   void plan(const std::vector<uint32_t> &w) { plan(w, {}, 1); }
-  void launch(hipStream_t s, const void *S);   // device xyzz[w.size()]
-  std::vector<hfp::Jac<HF>> read_windows(hipStream_t s);  // per-window sums, waits
+  void launch_head(hipStream_t s, const void *S, int set);  // level 0 (reads S = xyzz[w.size()])
+  void launch_tail(hipStream_t s, int set);                  // levels >= 1, dense, finalize
+  void launch(hipStream_t s, const void *S) {
+    launch_head(s, S, 0);
+    launch_tail(s, 0);
+  }
+  size_t out_bytes() const { return (size_t)2 * nwin_ * 144 * G; }
+  void copy_out(hipStream_t s, int set, void *host);               // async D2H of out_bytes()
+  std::vector<hfp::Jac<HF>> combine(const void *host) const;        // per-window sums
+  std::vector<hfp::Jac<HF>> read_windows(hipStream_t s);            // set 0, waits
   hfp::Jac<HF> read(hipStream_t s) { return read_windows(s)[0]; }
   size_t size() const { return bsize_; }
 
  private:
   size_t bsize_ = 0, final_perm_off_ = 0;
   int sbits_ = 1, nwin_ = 1;
-  DevBuf idx_, dense_buf_, part_[2];
+  DevBuf idx_, dense_buf_[NSETS], part_[NSETS][2];
   std::vector<DevBuf> starts_;
   std::vector<size_t> nout_;
-  ScanReducer<G> dense_;
+  ScanReducer<G> dense_[NSETS];
 };
 
 // Plain Pippenger bucket method (ref src/multi_scalar.c:549-576) on one GPU.
@@ -196,6 +205,10 @@ class Ches {
   void get_table(void *out_blst, size_t first, size_t count, hipStream_t s);
   // scalars: n 32-byte LE strings (stride >= 32) on device
   void run(hipStream_t s, const uint8_t *d_scalars, size_t stride, hfp::Jac<HF> *out);
+  // `count` MSMs over the same points; scalar set k at d_scalars + k * set_stride.
+  // Pipelined: MSM k's reduction tail runs on a second stream, beside MSM k+1.
+  void run_batch(hipStream_t s, const uint8_t *d_scalars, size_t stride, size_t set_stride, size_t count,
+                 hfp::Jac<HF> *outs);
   size_t npoints() const { return n_; }
   const ChesParams &params() const { return p_; }
   size_t bucket_count() const { return B_.size() + (size_t)(copies_ - 1) * small_; }
@@ -219,6 +232,12 @@ class Ches {
   BucketSort sort_;
   WeightedReducer<G> red_;
   std::vector<hipEvent_t> ev_;
+  hipStream_t tail_ = nullptr;
+  hipEvent_t ev_head_[2] = {nullptr, nullptr}, ev_tail_[2] = {nullptr, nullptr};
+  void *host_out_[2] = {nullptr, nullptr};
+  std::vector<hipEvent_t> acc_ev_;  // batch profiling: events around each accumulation
+  void front(hipStream_t s, const uint8_t *d_scalars, size_t stride, hipEvent_t acc0 = nullptr,
+             hipEvent_t acc1 = nullptr);  // digits, sort, accumulate
 };
 
 // device self-tests (engine.hip)
