@@ -126,6 +126,28 @@ int msm_ches_ctx_phase_times(const msm_ches_ctx *ctx, float out[6]);
 size_t msm_ches_ctx_bucket_count(const msm_ches_ctx *ctx);
 void msm_ches_ctx_destroy(msm_ches_ctx *ctx);
 
+/* ---- BGMW95 fixed-base method, device-resident precomputed table ----
+ * Replaces ref main_p1.cpp:94-122 init_pippenger_BGMW95 (table T[i h + j] = q^j P_i)
+ * and :294-398 pippenger_variant_BGMW95 (signed radix-q digits in (-q/2, q/2],
+ * r - s for large top digits, one set of q/2 buckets, tile
+ * blst_p1_tile_pippenger_BGMW95 multi_scalar.c:506-547 + integrate :281-297).
+ * q = 2^q_exp with q_exp * h >= 255; the reference's per-n choice is
+ * msm_ches_params(...)[7..8] (EXPONENT_OF_q_BGMW95, h_BGMW95). */
+typedef struct msm_bgmw_ctx msm_bgmw_ctx;
+int msm_bgmw_ctx_create(msm_bgmw_ctx **ctx, int group, int device, int q_exp, int h);
+int msm_bgmw_ctx_build_table(msm_bgmw_ctx *ctx, const void *points_affine, size_t npoints, int on_device,
+                             void *hip_stream);
+/* a precomputed T (blst affine, npoints * h entries, main_p1.cpp:109-119 order) */
+int msm_bgmw_ctx_set_table(msm_bgmw_ctx *ctx, const void *table_affine, size_t npoints, int on_device,
+                           void *hip_stream);
+int msm_bgmw_ctx_get_table(msm_bgmw_ctx *ctx, void *out_affine, size_t first, size_t count);
+int msm_bgmw_ctx_mult(msm_bgmw_ctx *ctx, void *ret, const byte *scalars, size_t stride, int scalars_on_device,
+                      void *hip_stream);
+int msm_bgmw_ctx_set_profiling(msm_bgmw_ctx *ctx, int on);
+int msm_bgmw_ctx_phase_times(const msm_bgmw_ctx *ctx, float out[6]);
+size_t msm_bgmw_ctx_bucket_count(const msm_bgmw_ctx *ctx);
+void msm_bgmw_ctx_destroy(msm_bgmw_ctx *ctx);
+
 /* host setup logic of the CHES method (no device work):
  * bucket set of ref auxiliaryfunc.h:257-288 (returns |B|; out may be NULL) */
 size_t msm_ches_bucket_set(int q, int a_h, int *out, size_t cap);

@@ -9,13 +9,15 @@ Mirrors:
   blst_p1s_mult_pippenger / blst_p2s_mult_pippenger  (ref bindings/blst.h:238-246, :377-384)
   MSMContext                                          device-resident points (extension)
   ches.CHESContext                                    ref main_p1.cpp CHES driver (see ches.py)
+  bgmw.BGMWContext                                    ref main_p1.cpp BGMW95 driver (see bgmw.py)
 """
 import ctypes
 
 from ._ffi import MsmError, check, lib
+from .bgmw import BGMWContext
 from .ches import CHESContext
 
-__all__ = ["MsmError", "MSMContext", "CHESContext", "p1s_mult_pippenger", "p2s_mult_pippenger", "fixed_points", "gen_scalars",
+__all__ = ["MsmError", "MSMContext", "CHESContext", "BGMWContext", "p1s_mult_pippenger", "p2s_mult_pippenger", "fixed_points", "gen_scalars",
            "compress", "to_affine", "device_count", "lib"]
 
 POINT_BYTES = {1: 96, 2: 192}

@@ -70,6 +70,17 @@ def lib():
     L.msm_ches_bucket_set.argtypes = [i32, i32, vp, sz]
     L.msm_ches_bucket_set.restype = sz
     L.msm_ches_digit_table.argtypes = [i32, i32, vp]
+    L.msm_bgmw_ctx_create.argtypes = [pp, i32, i32, i32, i32]
+    L.msm_bgmw_ctx_build_table.argtypes = [vp, vp, sz, i32, vp]
+    L.msm_bgmw_ctx_set_table.argtypes = [vp, vp, sz, i32, vp]
+    L.msm_bgmw_ctx_get_table.argtypes = [vp, vp, sz, sz]
+    L.msm_bgmw_ctx_mult.argtypes = [vp, vp, vp, sz, i32, vp]
+    L.msm_bgmw_ctx_set_profiling.argtypes = [vp, i32]
+    L.msm_bgmw_ctx_phase_times.argtypes = [vp, vp]
+    L.msm_bgmw_ctx_bucket_count.argtypes = [vp]
+    L.msm_bgmw_ctx_bucket_count.restype = sz
+    L.msm_bgmw_ctx_destroy.argtypes = [vp]
+    L.msm_bgmw_ctx_destroy.restype = None
     _lib = L
     return L
 

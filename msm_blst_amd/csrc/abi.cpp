@@ -168,6 +168,14 @@ struct msm_ches_ctx {
   DevBuf scalars;
 };
 
+struct msm_bgmw_ctx {
+  int group = 1;
+  int device = 0;
+  std::unique_ptr<Bgmw<1>> g1;
+  std::unique_ptr<Bgmw<2>> g2;
+  DevBuf scalars;
+};
+
 struct msm_ctx {
   int group = 1;
   int device = 0;
@@ -446,6 +454,99 @@ int msm_ches_ctx_phase_times(const msm_ches_ctx *ctx, float out[6]) {
 size_t msm_ches_ctx_bucket_count(const msm_ches_ctx *ctx) { return ctx ? CHES_DISPATCH(ctx, bucket_count()) : 0; }
 
 void msm_ches_ctx_destroy(msm_ches_ctx *ctx) { delete ctx; }
+
+// ---------------- BGMW95 contexts ----------------
+int msm_bgmw_ctx_create(msm_bgmw_ctx **ctx, int group, int device, int q_exp, int h) {
+  if (!ctx || (group != 1 && group != 2)) return fail(MSM_E_ARG, "bad ctx/group");
+  if (msm_device_count() <= device || device < 0) return fail(MSM_E_NODEV, "no such HIP device");
+  try {
+    auto c = std::make_unique<msm_bgmw_ctx>();
+    c->group = group;
+    c->device = device;
+    if (group == 1) c->g1 = std::make_unique<Bgmw<1>>(device, q_exp, h);
+    else c->g2 = std::make_unique<Bgmw<2>>(device, q_exp, h);
+    *ctx = c.release();
+    return MSM_OK;
+  } catch (const std::exception &e) {
+    return fail(MSM_E_ARG, e.what());
+  }
+}
+
+int msm_bgmw_ctx_build_table(msm_bgmw_ctx *ctx, const void *pts, size_t n, int on_device, void *stream) {
+  if (!ctx || (!pts && n)) return fail(MSM_E_ARG, "bad args");
+  try {
+    CHES_DISPATCH(ctx, build_table(pts, n, on_device != 0, (hipStream_t)stream));
+    return MSM_OK;
+  } catch (const std::exception &e) {
+    return fail(MSM_E_HIP, e.what());
+  }
+}
+
+int msm_bgmw_ctx_set_table(msm_bgmw_ctx *ctx, const void *tab, size_t n, int on_device, void *stream) {
+  if (!ctx || (!tab && n)) return fail(MSM_E_ARG, "bad args");
+  try {
+    CHES_DISPATCH(ctx, set_table(tab, n, on_device != 0, (hipStream_t)stream));
+    return MSM_OK;
+  } catch (const std::exception &e) {
+    return fail(MSM_E_HIP, e.what());
+  }
+}
+
+int msm_bgmw_ctx_get_table(msm_bgmw_ctx *ctx, void *out, size_t first, size_t count) {
+  if (!ctx || (!out && count)) return fail(MSM_E_ARG, "bad args");
+  try {
+    CHES_DISPATCH(ctx, get_table(out, first, count, (hipStream_t)0));
+    return MSM_OK;
+  } catch (const std::exception &e) {
+    return fail(MSM_E_HIP, e.what());
+  }
+}
+
+int msm_bgmw_ctx_mult(msm_bgmw_ctx *ctx, void *ret, const byte *scalars, size_t stride, int on_device,
+                      void *stream) {
+  if (!ctx || !ret || stride < 32) return fail(MSM_E_ARG, "bad args (stride must be >= 32)");
+  try {
+    DeviceGuard g(ctx->device);
+    hipStream_t s = (hipStream_t)stream;
+    size_t n = CHES_DISPATCH(ctx, npoints());
+    const uint8_t *d = scalars;
+    if (!on_device && n) {
+      ctx->scalars.ensure(n * stride + 16);
+      MSM_HIP_CHECK(hipMemcpyAsync(ctx->scalars.p, scalars, n * stride, hipMemcpyHostToDevice, s));
+      d = ctx->scalars.as<uint8_t>();
+    }
+    if (ctx->group == 1) {
+      hfp::Jac<hfp::Fp> out;
+      ctx->g1->run(s, d, stride, &out);
+      memcpy(ret, &out, sizeof out);
+    } else {
+      hfp::Jac<hfp::Fp2> out;
+      ctx->g2->run(s, d, stride, &out);
+      memcpy(ret, &out, sizeof out);
+    }
+    return MSM_OK;
+  } catch (const std::exception &e) {
+    return fail(MSM_E_HIP, e.what());
+  }
+}
+
+int msm_bgmw_ctx_set_profiling(msm_bgmw_ctx *ctx, int on) {
+  if (!ctx) return fail(MSM_E_ARG, "null ctx");
+  CHES_DISPATCH(ctx, set_profiling(on != 0));
+  return MSM_OK;
+}
+
+int msm_bgmw_ctx_phase_times(const msm_bgmw_ctx *ctx, float out[6]) {
+  if (!ctx || !out) return fail(MSM_E_ARG, "null");
+  const PhaseTimes &t = CHES_DISPATCH(ctx, times());
+  const float v[6] = {t.digits, t.sort, t.accumulate, t.reduce, t.finalize, t.total};
+  memcpy(out, v, sizeof v);
+  return MSM_OK;
+}
+
+size_t msm_bgmw_ctx_bucket_count(const msm_bgmw_ctx *ctx) { return ctx ? CHES_DISPATCH(ctx, bucket_count()) : 0; }
+
+void msm_bgmw_ctx_destroy(msm_bgmw_ctx *ctx) { delete ctx; }
 
 size_t msm_ches_bucket_set(int q, int a_h, int *out, size_t cap) {
   if (q < 4 || a_h < 0) return 0;

@@ -358,7 +358,7 @@ void Ches<G>::build_table(const void *pts, size_t n, bool on_device, hipStream_t
   pref.ensure(K * chunk * sizeof(F));
   for (size_t i0 = 0; i0 < n; i0 += chunk) {
     size_t cnt = std::min(chunk, n - i0);
-    hipLaunchKernelGGL(k_ches_table<G>, dim3(nblk(cnt, 64)), dim3(64), 0, s, base.as<Aff<F>>(), i0, cnt, p_.q_exp,
+    hipLaunchKernelGGL((k_ches_table<G, 3>), dim3(nblk(cnt, 64)), dim3(64), 0, s, base.as<Aff<F>>(), i0, cnt, p_.q_exp,
                        p_.h, scratch.as<Xyzz<F>>(), pref.as<F>(), table_.as<AffP<F>>());
     MSM_HIP_CHECK(hipGetLastError());
   }

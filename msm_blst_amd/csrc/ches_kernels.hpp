@@ -71,9 +71,11 @@ __device__ __forceinline__ void f_csub(Fp2 &a) {
 }
 
 // ------------------------------------------------------------ table build --
-// One lane per base point i in [i0, i0+cnt).  scratch holds the lane's 3h
+// One lane per base point i in [i0, i0+cnt).  scratch holds the lane's M h
 // xyzz points and prefix products, interleaved by lane for coalescing.
-template <int G>
+// M = 3: CHES table T[3(i h + j) + m - 1] = m q^j P_i (ref main_p1.cpp:155-172);
+// M = 1: BGMW95 table T[i h + j] = q^j P_i (ref main_p1.cpp:94-122).
+template <int G, int M = 3>
 static __global__ void __launch_bounds__(256)
     k_ches_table(const Aff<typename FieldOf<G>::F> *__restrict__ P, size_t i0, size_t cnt, int q_exp, int h,
                  Xyzz<typename FieldOf<G>::F> *__restrict__ scratch, typename FieldOf<G>::F *__restrict__ pref,
@@ -82,7 +84,8 @@ static __global__ void __launch_bounds__(256)
   size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= cnt) return;
   const size_t i = i0 + t;
-  const int K = 3 * h;
+  static_assert(M == 1 || M == 3, "M");
+  const int K = M * h;
   Aff<F> p = ld16(&P[i]);
   AffP<F> *out = T + (size_t)K * i;
   if (f_is_zero_exact(p.x) && f_is_zero_exact(p.y)) {  // infinity: every multiple is infinity
@@ -95,13 +98,15 @@ static __global__ void __launch_bounds__(256)
   Xyzz<F> Q;
   xyzz_from_aff(Q, p, false);
   for (int j = 0; j < h; ++j) {
-    Xyzz<F> Q2, Q3;
-    xyzz_dbl(Q2, Q);
-    Q3 = Q2;
-    xyzz_add(Q3, Q);
-    st16(&scratch[(size_t)(3 * j) * cnt + t], Q);
-    st16(&scratch[(size_t)(3 * j + 1) * cnt + t], Q2);
-    st16(&scratch[(size_t)(3 * j + 2) * cnt + t], Q3);
+    st16(&scratch[(size_t)(M * j) * cnt + t], Q);
+    if (M == 3) {
+      Xyzz<F> Q2, Q3;
+      xyzz_dbl(Q2, Q);
+      Q3 = Q2;
+      xyzz_add(Q3, Q);
+      st16(&scratch[(size_t)(3 * j + 1) * cnt + t], Q2);
+      st16(&scratch[(size_t)(3 * j + 2) * cnt + t], Q3);
+    }
     if (j + 1 < h)
       for (int e = 0; e < q_exp; ++e) {
         Xyzz<F> tmp = Q;
@@ -255,6 +260,82 @@ static __global__ void __launch_bounds__(256)
       carry = e >> 31;
       emit(j, e);
     }
+  }
+}
+
+// ----------------------------------------------------------- BGMW95 digits --
+// Signed radix-q digits in (-q/2, q/2] (ref auxiliaryfunc.h:130-145
+// trans_uint256_t_to_qhalf_expr): d_j = bits [j q_exp, (j+1) q_exp) plus the
+// carry; d_j > q/2 -> d_j - q, carry 1.  When the top digit would exceed q/2
+// the scalar is replaced by r - s and every digit negated (the reference's
+// "a > 0.5 q q^(h-1)" branch, main_p1.cpp:311-357, applied whenever it is
+// needed).  One entry per nonzero digit: key = |d| - 1 (bucket of value |d|),
+// val = table slot i h + j | sign << 31 (table T[i h + j] = q^j P_i).  Top-
+// digit entries with bucket < small go to copy i % copies of their bucket
+// (copy c >= 1 = nb0 + (c - 1) small + bucket), as in k_ches_digits.
+__device__ __forceinline__ void r_minus(uint32_t s[8]) {
+  int64_t br = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    int64_t d = (int64_t)FR_R32[k] - (int64_t)s[k] + br;
+    s[k] = (uint32_t)d;
+    br = d >> 32;
+  }
+}
+static __global__ void __launch_bounds__(256)
+    k_bgmw_digits(const uint8_t *__restrict__ scalars, size_t stride, size_t n, int q_exp, int h,
+                  uint32_t *__restrict__ keys, uint32_t *__restrict__ vals, uint32_t nb0, uint32_t small,
+                  uint32_t copies) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t *sp = scalars + i * stride;
+  uint32_t s[10];
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+    s[k] = (stride & 3) == 0 ? reinterpret_cast<const uint32_t *>(sp)[k]
+                             : (uint32_t)sp[4 * k] | ((uint32_t)sp[4 * k + 1] << 8) |
+                                   ((uint32_t)sp[4 * k + 2] << 16) | ((uint32_t)sp[4 * k + 3] << 24);
+  sub_r_if_ge(s);
+  sub_r_if_ge(s);
+  s[8] = s[9] = 0;
+  const int32_t q = 1 << q_exp, qh = q >> 1;
+  const uint32_t qmask = (uint32_t)q - 1u;
+  auto digit = [&](int j) -> int32_t {
+    int off = j * q_exp;
+    int wi = off >> 5, sh = off & 31;
+    uint32_t lo = wi < 10 ? s[wi] : 0u, hi = wi + 1 < 10 ? s[wi + 1] : 0u;
+    return (int32_t)((uint32_t)((((uint64_t)hi << 32) | lo) >> sh) & qmask);
+  };
+  // top digit after carries: > q/2 exactly when the carry-propagated value of
+  // the top digit is; run the carry chain once to decide, then emit
+  int32_t carry = 0;
+  for (int j = 0; j < h - 1; ++j) carry = digit(j) + carry > qh ? 1 : 0;
+  uint32_t neg = 0;
+  if (digit(h - 1) + carry > qh) {
+    r_minus(s);
+    neg = 1u;
+  }
+  carry = 0;
+  for (int j = 0; j < h; ++j) {
+    int32_t d = digit(j) + carry;
+    carry = 0;
+    if (j < h - 1 && d > qh) {
+      d -= q;
+      carry = 1;
+    }
+    const size_t k = (size_t)j * n + i;
+    if (d == 0) {
+      keys[k] = KEY_NONE;
+      continue;
+    }
+    uint32_t sign = (d < 0 ? 1u : 0u) ^ neg;
+    uint32_t b = (uint32_t)(d < 0 ? -d : d) - 1u;
+    if (j == h - 1 && b < small) {
+      uint32_t c = (uint32_t)(i % copies);
+      if (c) b = nb0 + (c - 1) * small + b;
+    }
+    keys[k] = b;
+    vals[k] = (uint32_t)(i * (size_t)h + j) | (sign << 31);
   }
 }
 

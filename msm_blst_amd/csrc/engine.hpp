@@ -240,6 +240,43 @@ class Ches {
              hipEvent_t acc1 = nullptr);  // digits, sort, accumulate
 };
 
+// BGMW95 fixed-base variant (ref main_p1.cpp:94-122, 294-398;
+// multi_scalar.c:506-547): table T[i h + j] = q^j P_i resident in HBM, signed
+// radix-q digits in (-q/2, q/2], all n h digits accumulated into ONE set of
+// q/2 buckets, then sum_b b S_b.  (bgmw.hip)
+template <int G>
+class Bgmw {
+ public:
+  typedef typename HostField<G>::F HF;
+  Bgmw(int device, int q_exp, int h);
+  ~Bgmw();
+  void build_table(const void *points_blst, size_t n, bool on_device, hipStream_t s);
+  void set_table(const void *table_blst, size_t n, bool on_device, hipStream_t s);  // n h points
+  void get_table(void *out_blst, size_t first, size_t count, hipStream_t s);
+  // scalars: n 32-byte LE strings (stride >= 32) on device
+  void run(hipStream_t s, const uint8_t *d_scalars, size_t stride, hfp::Jac<HF> *out);
+  size_t npoints() const { return n_; }
+  int q_exp() const { return q_exp_; }
+  int h() const { return h_; }
+  size_t bucket_count() const { return nb0_ + (size_t)(copies_ - 1) * small_; }
+  void set_profiling(bool on) { profile_ = on; }
+  const PhaseTimes &times() const { return times_; }
+  int device() const { return dev_; }
+
+ private:
+  int dev_, q_exp_, h_;
+  size_t n_ = 0, nb0_ = 0;
+  uint32_t small_ = 0;
+  int copies_ = 1;
+  bool profile_ = false;
+  PhaseTimes times_;
+  DevBuf table_, keys_, vals_, counts_, offsets_, sorted_, order_, buckets_;
+  BucketSort sort_;
+  WeightedReducer<G> red_;
+  std::vector<hipEvent_t> ev_;
+  void plan_buckets(size_t n);
+};
+
 // device self-tests (engine.hip)
 template <int G>
 void test_field(int op, const uint64_t *a, const uint64_t *b, uint64_t *out, size_t n);
