@@ -107,7 +107,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--log-n", type=int, default=20, help="points per GPU = 2^log_n")
-    ap.add_argument("--method", choices=("ches", "pippenger"), default="ches")
+    ap.add_argument("--method", choices=("ches", "pippenger", "bgmw"), default="ches")
     ap.add_argument("--window", type=int, default=16, help="plain Pippenger window bits")
     ap.add_argument("--no-compare", action="store_true", help="skip timing the other method (N = 1)")
     ap.add_argument("--no-batch", action="store_true",
@@ -160,6 +160,12 @@ def main():
                 return ctx.mult_batch(d_sc.data_ptr(), k, 32, set_stride=0, on_device=True,
                                       stream=stream.cuda_stream)
             ctx._bench_batch = mult_batch
+        elif method == "bgmw":
+            ctx = m.BGMWContext(1, local, n_exp=args.log_n)
+            ctx.build_table(pts, n, stream=stream.cuda_stream)
+
+            def mult():
+                return ctx.mult(d_sc.data_ptr(), 32, on_device=True, stream=stream.cuda_stream)
         else:
             ctx = m.MSMContext(1, local, args.window)
             ctx.set_points(pts, n, stream=stream.cuda_stream)
@@ -197,16 +203,19 @@ def main():
                 "ms_per_step": round(sel / args.steps * 1e3, 4),
                 "parity_vs_reference": (m.compress(1, sres).hex() == want[0]) if want else None,
                 "note": "K synchronous msm_ches_ctx_mult calls (per-MSM latency)"}
-    other = None
-    if world == 1 and not args.no_compare:
-        ometh = "pippenger" if args.method == "ches" else "ches"
-        octx, ostep = make(ometh)
-        ores, oel, oacc, _, oph = timed_steps(ostep, octx, max(5, args.steps // 2), 2, world, dev)
-        other = {"method": ometh, "value": round(n * max(5, args.steps // 2) / oel, 1), "unit": "pairs/s",
-                 "ms_per_step": round(oel / max(5, args.steps // 2) * 1e3, 4),
-                 "phases_ms": {k: round(v, 4) for k, v in oph.items()},
-                 "parity_vs_reference": (m.compress(1, ores).hex() == want[0]) if want else None}
-        octx.close()
+    others = {}
+    if world == 1 and not args.no_compare:  # the reference's other methods, same points and scalars
+        for ometh in ("ches", "pippenger", "bgmw"):
+            if ometh == args.method:
+                continue
+            octx, ostep = make(ometh)
+            k = max(5, args.steps // 2)
+            ores, oel, oacc, _, oph = timed_steps(ostep, octx, k, 2, world, dev)
+            others[ometh] = {"value": round(n * k / oel, 1), "unit": "pairs/s",
+                             "ms_per_step": round(oel / k * 1e3, 4),
+                             "phases_ms": {kk: round(v, 4) for kk, v in oph.items()},
+                             "parity_vs_reference": (m.compress(1, ores).hex() == want[0]) if want else None}
+            octx.close()
 
     if rank != 0:
         if world > 1:
@@ -223,6 +232,13 @@ def main():
                     f"|B|={ctx.params['b_size']}), table T=m*q^j*P_i resident in HBM, scalars resident in HBM")
         cfg_extra = {"method": "ches_q_over_5", "q_exp": ctx.params["q_exp"], "h": h,
                      "bucket_set": ctx.params["b_size"], "buckets_incl_top_digit_copies": ctx.bucket_count()}
+    elif args.method == "bgmw":
+        h = ctx.h
+        madds = n * h
+        alg_bytes = n * h * AFFINE_BYTES
+        workload = (f"G1 MSM n=2^{args.log_n} per GPU, BGMW95 (q=2^{ctx.q_exp}, h={h}), table q^j*P_i resident in HBM, "
+                    f"scalars resident in HBM")
+        cfg_extra = {"method": "bgmw95", "q_exp": ctx.q_exp, "h": h}
     else:
         W = (255 + 1 + args.window - 1) // args.window
         madds = n * W
@@ -277,7 +293,7 @@ def main():
         "methods": {args.method + ("_batch" if batched else ""): {"value": round(value, 1),
                                                                    "ms_per_step": round(elapsed / args.steps * 1e3, 4)},
                     **({"ches_sync": sync} if sync else {}),
-                    **({other["method"]: other} if other else {})},
+                    **others},
         "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)

@@ -61,6 +61,84 @@ void blst_p2s_tile_pippenger(blst_p2 *ret, const blst_p2_affine *const points[],
                              const byte *const scalars[], size_t nbits, limb_t *scratch, size_t bit0,
                              size_t window);
 
+/* ---- blst-level CHES / BGMW95 entry points (replace ref src/multi_scalar.c:584-790,
+ * declared at ref bindings/blst.h:249-357; used by ref main_p1.cpp:233-236, :279-282, :384) ----
+ * Same names, argument meaning and layouts.  The tile_* and integrate_* calls run on
+ * the GPU (entries uploaded, sorted by bucket, accumulated one lane per bucket, then
+ * the weighted bucket sum); the per-point helpers run on the host (one point op is
+ * far below a kernel launch).  Differences, all toward the mathematically exact sum:
+ * the last-element guard of ref multi_scalar.c:461 is applied to the last element's
+ * own bucket (SURVEY 8a defect 1); buckets[] is filled with the per-bucket sums as
+ * the reference leaves it (xyzz representatives may differ; equal as points). */
+size_t blst_p1s_mult_pippenger_scratch_sizeof_CHES(size_t window);  /* multi_scalar.c:584-585 */
+size_t blst_p2s_mult_pippenger_scratch_sizeof_CHES(size_t window);
+void blst_p1xyzz_dadd_affine(blst_p1xyzz *out, const blst_p1xyzz *in, const blst_p1_affine *p,
+                             unsigned char booth_sign);              /* ec_ops.h:710-769 */
+void blst_p2xyzz_dadd_affine(blst_p2xyzz *out, const blst_p2xyzz *in, const blst_p2_affine *p,
+                             unsigned char booth_sign);
+void blst_p1xyzz_dadd(blst_p1xyzz *p3, const blst_p1xyzz *p1, const blst_p1xyzz *p2);  /* ec_ops.h:642-702 */
+void blst_p2xyzz_dadd(blst_p2xyzz *p3, const blst_p2xyzz *p1, const blst_p2xyzz *p2);
+void blst_p1xyzz_to_Jacobian(blst_p1 *out, const blst_p1xyzz *in);   /* ec_ops.h:771-777 */
+void blst_p2xyzz_to_Jacobian(blst_p2 *out, const blst_p2xyzz *in);
+void blst_p1_to_xyzz(blst_p1xyzz *out, blst_p1 *in);                /* ec_ops.h:779-785 */
+void blst_p2_to_xyzz(blst_p2xyzz *out, blst_p2 *in);
+void blst_p1_prefetch_CHES(const blst_p1xyzz buckets[], size_t booth_idx);  /* no-op hint */
+void blst_p2_prefetch_CHES(const blst_p2xyzz buckets[], size_t booth_idx);
+void blst_p1_bucket_CHES(blst_p1xyzz buckets[], int booth_idx, const blst_p1_affine *p,
+                         unsigned char booth_sign);                  /* multi_scalar.c:358-361 */
+void blst_p2_bucket_CHES(blst_p2xyzz buckets[], int booth_idx, const blst_p2_affine *p, unsigned char booth_sign);
+/* sum_i bucket_set_ascend[i] * buckets[i] (multi_scalar.c:301-321); any non-negative
+ * weights are accepted (d_max is not needed by the GPU reduction) */
+void blst_p1_integrate_buckets_accumulation_d_CHES(blst_p1 *out, blst_p1xyzz buckets[], int bucket_set_ascend[],
+                                                   size_t bucket_set_size, int d_max);
+void blst_p2_integrate_buckets_accumulation_d_CHES(blst_p2 *out, blst_p2xyzz buckets[], int bucket_set_ascend[],
+                                                   size_t bucket_set_size, int d_max);
+/* integral scalar conversion (multi_scalar.c:748-775): standard q-ary digits in
+ * nh_scalars[] (carry written into the next slot) -> bucket values, signs, table pointers */
+void blst_p1_construct_nh_scalars_nh_points(int nh_scalars[], unsigned char booth_signs[],
+                                            blst_p1_affine *nh_points_ptr[], const size_t npoints,
+                                            blst_p1_affine precomputation_points_list_3nh[],
+                                            const digit_decomposition digit_conversion_hash_table[]);
+void blst_p2_construct_nh_scalars_nh_points(int nh_scalars[], unsigned char booth_signs[],
+                                            blst_p2_affine *nh_points_ptr[], const size_t npoints,
+                                            blst_p2_affine precomputation_points_list_3nh[],
+                                            const digit_decomposition digit_conversion_hash_table[]);
+/* CHES accumulation + d-reduction (multi_scalar.c:421-463, 643-655) */
+void blst_p1_tile_pippenger_d_CHES(blst_p1 *ret, const blst_p1_affine *const points[], size_t npoints,
+                                   const int scalars[], const unsigned char booth_signs[], blst_p1xyzz buckets[],
+                                   int bucket_set_ascend[], int bucket_value_to_its_index[], size_t bucket_set_size,
+                                   int d_max);
+void blst_p2_tile_pippenger_d_CHES(blst_p2 *ret, const blst_p2_affine *const points[], size_t npoints,
+                                   const int scalars[], const unsigned char booth_signs[], blst_p2xyzz buckets[],
+                                   int bucket_set_ascend[], int bucket_value_to_its_index[], size_t bucket_set_size,
+                                   int d_max);
+/* buckets indexed by bucket value (multi_scalar.c:466-503); values outside the set weigh 0 */
+void blst_p1_tile_pippenger_d_CHES_noindexhash(blst_p1 *ret, const blst_p1_affine *const points[], size_t npoints,
+                                               const int scalars[], const unsigned char booth_signs[],
+                                               blst_p1xyzz buckets[], int bucket_set_ascend[], size_t bucket_set_size,
+                                               int d_max);
+void blst_p2_tile_pippenger_d_CHES_noindexhash(blst_p2 *ret, const blst_p2_affine *const points[], size_t npoints,
+                                               const int scalars[], const unsigned char booth_signs[],
+                                               blst_p2xyzz buckets[], int bucket_set_ascend[], size_t bucket_set_size,
+                                               int d_max);
+/* standard q-ary digits in, digit-hash lookup + carry inside (multi_scalar.c:671-744);
+ * scalars[] is updated with the carries as the reference does (needs one slot of padding) */
+void blst_p1_tile_pippenger_CHES_prefetch_2step_ahead_input_std_scalar(
+    blst_p1 *ret, const blst_p1_affine precomputation_points_list_3nh[], size_t npoints, int scalars[],
+    digit_decomposition digit_conversion_hash_table[], blst_p1xyzz buckets[], int bucket_set_ascend[],
+    int bucket_value_to_its_index[], size_t bucket_set_size, int d_max);
+void blst_p2_tile_pippenger_CHES_prefetch_2step_ahead_input_std_scalar(
+    blst_p2 *ret, const blst_p2_affine precomputation_points_list_3nh[], size_t npoints, int scalars[],
+    digit_decomposition digit_conversion_hash_table[], blst_p2xyzz buckets[], int bucket_set_ascend[],
+    int bucket_value_to_its_index[], size_t bucket_set_size, int d_max);
+/* BGMW95 accumulation + running-sum reduction (multi_scalar.c:506-547); |digits| <= q/2 */
+void blst_p1_tile_pippenger_BGMW95(blst_p1 *ret, const blst_p1_affine *const points[], size_t npoints,
+                                   const int scalars[], const unsigned char booth_signs[], blst_p1xyzz buckets[],
+                                   size_t q_exponent);
+void blst_p2_tile_pippenger_BGMW95(blst_p2 *ret, const blst_p2_affine *const points[], size_t npoints,
+                                   const int scalars[], const unsigned char booth_signs[], blst_p2xyzz buckets[],
+                                   size_t q_exponent);
+
 /* ---- extension API: device-resident contexts (points uploaded once) ---- */
 enum {
   MSM_OK = 0,

@@ -143,6 +143,90 @@ void tile_pippenger(void *ret, const void *const *points, size_t n, const byte *
   memcpy(ret, &out, sizeof out);
 }
 
+// ---- blst-level CHES / BGMW95 tiles (ref multi_scalar.c:421-547, 671-744) ----
+constexpr uint32_t kNone = 0xffffffffu;  // entry skipped (bucket sort key)
+// gather the per-entry point pointers into one flat host array
+template <int G>
+void gather_ptrs(std::vector<uint8_t> &flat, const void *const *points, size_t n) {
+  const size_t psz = 96 * G;
+  flat.resize(n * psz);
+  for (size_t t = 0; t < n; ++t) memcpy(flat.data() + t * psz, points[t], psz);
+}
+
+// ref multi_scalar.c:421-463: entry t -> bucket v2i[scalars[t]] (0 = skipped),
+// weight of bucket k = bucket_set_ascend[k]
+template <int G>
+void tile_d_ches(void *ret, const void *const *points, size_t n, const int *scalars, const unsigned char *signs,
+                 void *buckets, const int *B, const int *v2i, size_t bsize) {
+  std::vector<uint8_t> flat;
+  gather_ptrs<G>(flat, points, n);
+  std::vector<uint32_t> keys(n), vals(n), w(bsize);
+  for (size_t t = 0; t < n; ++t) {
+    int idx = v2i[scalars[t]];
+    keys[t] = idx > 0 ? (uint32_t)idx : kNone;
+    vals[t] = (uint32_t)t | ((uint32_t)(signs[t] != 0) << 31);
+  }
+  for (size_t k = 0; k < bsize; ++k) w[k] = (uint32_t)std::max(B[k], 0);
+  entry_msm<G>(ret, flat.data(), n, keys.data(), vals.data(), n, bsize, w.data(), buckets);
+}
+
+// ref multi_scalar.c:466-503: buckets indexed by value; weight v for v in B, else 0
+template <int G>
+void tile_d_ches_noindex(void *ret, const void *const *points, size_t n, const int *scalars,
+                         const unsigned char *signs, void *buckets, const int *B, size_t bsize) {
+  if (bsize == 0) throw std::runtime_error("empty bucket set");
+  const size_t nb = (size_t)B[bsize - 1] + 1;
+  std::vector<uint8_t> flat;
+  gather_ptrs<G>(flat, points, n);
+  std::vector<uint32_t> keys(n), vals(n), w(nb, 0);
+  for (size_t k = 1; k < bsize; ++k) w[B[k]] = (uint32_t)B[k];
+  for (size_t t = 0; t < n; ++t) {
+    int v = scalars[t];
+    if (v < 0 || (size_t)v >= nb) throw std::runtime_error("bucket value outside the bucket set range");
+    keys[t] = v > 0 ? (uint32_t)v : kNone;
+    vals[t] = (uint32_t)t | ((uint32_t)(signs[t] != 0) << 31);
+  }
+  entry_msm<G>(ret, flat.data(), n, keys.data(), vals.data(), n, nb, w.data(), buckets);
+}
+
+// ref multi_scalar.c:671-744: standard q-ary digits, hash lookup and carry
+// (written back into scalars[t + 1]) here, table slots 3 t + m - 1
+template <int G>
+void tile_ches_std(void *ret, const void *table, size_t n, int *scalars, const digit_decomposition *H, void *buckets,
+                   const int *B, const int *v2i, size_t bsize) {
+  std::vector<uint32_t> keys(n), vals(n), w(bsize);
+  for (size_t t = 0; t < n; ++t) {
+    const digit_decomposition d = H[scalars[t]];
+    if (d.alpha) ++scalars[t + 1];
+    int idx = v2i[d.b];
+    keys[t] = idx > 0 ? (uint32_t)idx : kNone;
+    vals[t] = (uint32_t)(3 * t + d.m - 1) | ((uint32_t)(d.alpha != 0) << 31);
+  }
+  for (size_t k = 0; k < bsize; ++k) w[k] = (uint32_t)std::max(B[k], 0);
+  entry_msm<G>(ret, table, 3 * n, keys.data(), vals.data(), n, bsize, w.data(), buckets);
+}
+
+// ref multi_scalar.c:506-547: bucket value v in [1, q/2] -> bucket v - 1 of weight v
+template <int G>
+void tile_bgmw95(void *ret, const void *const *points, size_t n, const int *scalars, const unsigned char *signs,
+                 void *buckets, size_t q_exp) {
+  if (q_exp < 2 || q_exp > 26) throw std::runtime_error("q_exponent out of range");
+  const size_t nb = (size_t)1 << (q_exp - 1);
+  std::vector<uint8_t> flat;
+  gather_ptrs<G>(flat, points, n);
+  std::vector<uint32_t> keys(n), vals(n), w(nb);
+  for (size_t k = 0; k < nb; ++k) w[k] = (uint32_t)(k + 1);
+  for (size_t t = 0; t < n; ++t) {
+    int v = scalars[t];
+    if (v < 0 || (size_t)v > nb) throw std::runtime_error("BGMW95 digit outside [0, q/2]");
+    keys[t] = v > 0 ? (uint32_t)(v - 1) : kNone;
+    vals[t] = (uint32_t)t | ((uint32_t)(signs[t] != 0) << 31);
+  }
+  entry_msm<G>(ret, flat.data(), n, keys.data(), vals.data(), n, nb, w.data(), nullptr);
+  // the reference's integrate_buckets leaves buckets[0 .. q/2] zeroed
+  if (buckets) memset(buckets, 0, (nb + 1) * 192 * G);
+}
+
 size_t blst_window(size_t n) {  // ref multi_scalar.c:268-275
   size_t w = 0;
   while (n >>= 1) ++w;
@@ -225,6 +309,112 @@ void blst_p2s_tile_pippenger(blst_p2 *ret, const blst_p2_affine *const points[],
     die("blst_p2s_tile_pippenger", e);
   }
 }
+
+// ---- blst-level CHES / BGMW95 entry points ----
+size_t blst_p1s_mult_pippenger_scratch_sizeof_CHES(size_t window) { return sizeof(blst_p1xyzz) * (window / 2); }
+size_t blst_p2s_mult_pippenger_scratch_sizeof_CHES(size_t window) { return sizeof(blst_p2xyzz) * (window / 2); }
+
+#define MSM_XYZZ_HELPERS(g, F)                                                                                   \
+  void blst_p##g##xyzz_dadd_affine(blst_p##g##xyzz *out, const blst_p##g##xyzz *in, const blst_p##g##_affine *p, \
+                                   unsigned char booth_sign) {                                                   \
+    *reinterpret_cast<hfp::Xyzz<F> *>(out) = hfp::xyzz_madd(*reinterpret_cast<const hfp::Xyzz<F> *>(in),         \
+                                                            *reinterpret_cast<const hfp::Aff<F> *>(p),           \
+                                                            booth_sign != 0);                                    \
+  }                                                                                                              \
+  void blst_p##g##xyzz_dadd(blst_p##g##xyzz *p3, const blst_p##g##xyzz *p1, const blst_p##g##xyzz *p2) {         \
+    *reinterpret_cast<hfp::Xyzz<F> *>(p3) = hfp::xyzz_add(*reinterpret_cast<const hfp::Xyzz<F> *>(p1),           \
+                                                          *reinterpret_cast<const hfp::Xyzz<F> *>(p2));          \
+  }                                                                                                              \
+  void blst_p##g##xyzz_to_Jacobian(blst_p##g *out, const blst_p##g##xyzz *in) {                                  \
+    *reinterpret_cast<hfp::Jac<F> *>(out) = hfp::xyzz_to_jac(*reinterpret_cast<const hfp::Xyzz<F> *>(in));       \
+  }                                                                                                              \
+  void blst_p##g##_to_xyzz(blst_p##g##xyzz *out, blst_p##g *in) {                                                \
+    *reinterpret_cast<hfp::Xyzz<F> *>(out) = hfp::jac_to_xyzz(*reinterpret_cast<const hfp::Jac<F> *>(in));       \
+  }                                                                                                              \
+  void blst_p##g##_prefetch_CHES(const blst_p##g##xyzz buckets[], size_t booth_idx) {                            \
+    (void)buckets;                                                                                               \
+    (void)booth_idx;                                                                                             \
+  }                                                                                                              \
+  void blst_p##g##_bucket_CHES(blst_p##g##xyzz buckets[], int booth_idx, const blst_p##g##_affine *p,            \
+                               unsigned char booth_sign) {                                                       \
+    blst_p##g##xyzz_dadd_affine(&buckets[booth_idx], &buckets[booth_idx], p, booth_sign);                        \
+  }
+MSM_XYZZ_HELPERS(1, hfp::Fp)
+MSM_XYZZ_HELPERS(2, hfp::Fp2)
+#undef MSM_XYZZ_HELPERS
+
+#define MSM_CHES_ENTRIES(g)                                                                                        \
+  void blst_p##g##_integrate_buckets_accumulation_d_CHES(blst_p##g *out, blst_p##g##xyzz buckets[],              \
+                                                         int bucket_set_ascend[], size_t bucket_set_size,         \
+                                                         int d_max) {                                             \
+    (void)d_max;                                                                                                  \
+    try {                                                                                                         \
+      std::vector<uint32_t> w(bucket_set_size);                                                                   \
+      for (size_t k = 0; k < bucket_set_size; ++k) w[k] = (uint32_t)std::max(bucket_set_ascend[k], 0);           \
+      weighted_bucket_sum<g>(out, buckets, bucket_set_size, w.data());                                            \
+    } catch (const std::exception &e) {                                                                           \
+      die("blst_p" #g "_integrate_buckets_accumulation_d_CHES", e);                                               \
+    }                                                                                                             \
+  }                                                                                                               \
+  void blst_p##g##_construct_nh_scalars_nh_points(int nh_scalars[], unsigned char booth_signs[],                  \
+                                                  blst_p##g##_affine *nh_points_ptr[], const size_t npoints,     \
+                                                  blst_p##g##_affine table[], const digit_decomposition H[]) {   \
+    for (size_t i = 0; i < npoints; ++i) {                                                                        \
+      const digit_decomposition d = H[nh_scalars[i]];                                                             \
+      nh_scalars[i] = d.b;                                                                                        \
+      booth_signs[i] = (unsigned char)d.alpha;                                                                    \
+      if (d.alpha && i + 1 < npoints) ++nh_scalars[i + 1];                                                        \
+      nh_points_ptr[i] = table + 3 * i + d.m - 1;                                                                 \
+    }                                                                                                             \
+  }                                                                                                               \
+  void blst_p##g##_tile_pippenger_d_CHES(blst_p##g *ret, const blst_p##g##_affine *const points[], size_t npoints, \
+                                         const int scalars[], const unsigned char booth_signs[],                  \
+                                         blst_p##g##xyzz buckets[], int bucket_set_ascend[],                      \
+                                         int bucket_value_to_its_index[], size_t bucket_set_size, int d_max) {    \
+    (void)d_max;                                                                                                  \
+    try {                                                                                                         \
+      tile_d_ches<g>(ret, (const void *const *)points, npoints, scalars, booth_signs, buckets, bucket_set_ascend, \
+                     bucket_value_to_its_index, bucket_set_size);                                                 \
+    } catch (const std::exception &e) {                                                                           \
+      die("blst_p" #g "_tile_pippenger_d_CHES", e);                                                               \
+    }                                                                                                             \
+  }                                                                                                               \
+  void blst_p##g##_tile_pippenger_d_CHES_noindexhash(                                                             \
+      blst_p##g *ret, const blst_p##g##_affine *const points[], size_t npoints, const int scalars[],               \
+      const unsigned char booth_signs[], blst_p##g##xyzz buckets[], int bucket_set_ascend[],                      \
+      size_t bucket_set_size, int d_max) {                                                                        \
+    (void)d_max;                                                                                                  \
+    try {                                                                                                         \
+      tile_d_ches_noindex<g>(ret, (const void *const *)points, npoints, scalars, booth_signs, buckets,            \
+                             bucket_set_ascend, bucket_set_size);                                                 \
+    } catch (const std::exception &e) {                                                                           \
+      die("blst_p" #g "_tile_pippenger_d_CHES_noindexhash", e);                                                   \
+    }                                                                                                             \
+  }                                                                                                               \
+  void blst_p##g##_tile_pippenger_CHES_prefetch_2step_ahead_input_std_scalar(                                     \
+      blst_p##g *ret, const blst_p##g##_affine table[], size_t npoints, int scalars[],                            \
+      digit_decomposition H[], blst_p##g##xyzz buckets[], int bucket_set_ascend[],                                \
+      int bucket_value_to_its_index[], size_t bucket_set_size, int d_max) {                                       \
+    (void)d_max;                                                                                                  \
+    try {                                                                                                         \
+      tile_ches_std<g>(ret, table, npoints, scalars, H, buckets, bucket_set_ascend, bucket_value_to_its_index,    \
+                       bucket_set_size);                                                                          \
+    } catch (const std::exception &e) {                                                                           \
+      die("blst_p" #g "_tile_pippenger_CHES_prefetch_2step_ahead_input_std_scalar", e);                           \
+    }                                                                                                             \
+  }                                                                                                               \
+  void blst_p##g##_tile_pippenger_BGMW95(blst_p##g *ret, const blst_p##g##_affine *const points[], size_t npoints, \
+                                         const int scalars[], const unsigned char booth_signs[],                  \
+                                         blst_p##g##xyzz buckets[], size_t q_exponent) {                          \
+    try {                                                                                                         \
+      tile_bgmw95<g>(ret, (const void *const *)points, npoints, scalars, booth_signs, buckets, q_exponent);       \
+    } catch (const std::exception &e) {                                                                           \
+      die("blst_p" #g "_tile_pippenger_BGMW95", e);                                                               \
+    }                                                                                                             \
+  }
+MSM_CHES_ENTRIES(1)
+MSM_CHES_ENTRIES(2)
+#undef MSM_CHES_ENTRIES
 
 const char *msm_last_error(void) { return g_err.c_str(); }
 

@@ -410,3 +410,25 @@ __global__ void k_import_xyzz(const uint64_t *__restrict__ in, Xyzz<typename Fie
 }
 
 }  // namespace msm
+
+namespace msm {
+// internal xyzz -> blst xyzz {x, y, zzz, zz} (Montgomery R=2^384, canonical);
+// infinity -> all zero
+template <int G>
+__global__ void k_export_xyzz(const Xyzz<typename FieldOf<G>::F> *__restrict__ in, uint64_t *__restrict__ out,
+                              size_t n) {
+  typedef typename FieldOf<G>::F F;
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Xyzz<F> a = ld16(&in[i]);
+  uint64_t *o = out + i * 24 * G;
+  if (xyzz_is_inf(a)) {
+    for (int k = 0; k < 24 * G; ++k) o[k] = 0;
+    return;
+  }
+  f_to_blst(o, a.x);
+  f_to_blst(o + 6 * G, a.y);
+  f_to_blst(o + 12 * G, a.zzz);
+  f_to_blst(o + 18 * G, a.zz);
+}
+}  // namespace msm

@@ -277,6 +277,17 @@ class Bgmw {
   void plan_buckets(size_t n);
 };
 
+// blst-level tile entry points (compat.hip): sum_b weights[b] * (sum of the
+// entries of bucket b), entries (keys[k] = bucket or KEY_NONE, vals[k] = point
+// index | sign << 31) over npts blst affine points in host memory; bucket sums
+// optionally written back in blst xyzz layout to host memory buckets_out.
+template <int G>
+void entry_msm(void *ret_jac, const void *pts_blst, size_t npts, const uint32_t *keys, const uint32_t *vals,
+               size_t ne, size_t nb, const uint32_t *weights, void *buckets_out);
+// sum_i weights[i] * buckets[i] for nb blst xyzz buckets in host memory
+template <int G>
+void weighted_bucket_sum(void *ret_jac, const void *buckets_blst, size_t nb, const uint32_t *weights);
+
 // device self-tests (engine.hip)
 template <int G>
 void test_field(int op, const uint64_t *a, const uint64_t *b, uint64_t *out, size_t n);

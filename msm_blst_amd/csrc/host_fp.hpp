@@ -253,6 +253,97 @@ void to_affine_batch(Aff<F> *out, const Jac<F> *in, size_t n) {
   }
 }
 
+// ---- xyzz points (layout of blst_p1xyzz / blst_p2xyzz: x, y, zzz, zz) ----
+// Host restatements of the single-point bucket helpers the reference exports
+// (ref src/ec_ops.h:642-785, multi_scalar.c:609-641).  They serve the per-point
+// blst_p*xyzz_* boundary functions only; bucket accumulation runs on the GPU.
+template <class F>
+struct Xyzz {
+  F x, y, zzz, zz;
+};
+template <class F>
+bool xyzz_is_inf(const Xyzz<F> &a) {
+  return is_zero(a.zzz) && is_zero(a.zz);
+}
+// mdbl-2008-s-1 of the affine point (x, y)
+template <class F>
+Xyzz<F> xyzz_dbl_aff(const F &x, const F &y) {
+  Xyzz<F> r;
+  F U = add(y, y);
+  r.zz = mul(U, U);
+  r.zzz = mul(r.zz, U);
+  F S = mul(x, r.zz);
+  F M = mul(x, x);
+  M = add(add(M, M), M);
+  r.x = sub(sub(mul(M, M), S), S);
+  r.y = sub(mul(sub(S, r.x), M), mul(r.zzz, y));
+  return r;
+}
+// p1 + (subtract ? -p2 : p2)   (ref ec_ops.h:710-769, madd-2008-s with twists)
+template <class F>
+Xyzz<F> xyzz_madd(const Xyzz<F> &p1, const Aff<F> &p2, bool subtract) {
+  if (is_zero(p2.x) && is_zero(p2.y)) return p1;
+  const F one = fone(F());
+  if (xyzz_is_inf(p1)) {
+    Xyzz<F> r{p2.x, p2.y, subtract ? neg(one) : one, one};
+    return r;
+  }
+  F P = sub(mul(p2.x, p1.zz), p1.x);
+  F R = mul(p2.y, p1.zzz);
+  if (subtract) R = neg(R);
+  R = sub(R, p1.y);
+  Xyzz<F> r;
+  if (!is_zero(P)) {
+    F PP = mul(P, P), PPP = mul(PP, P), Q = mul(p1.x, PP);
+    r.x = sub(sub(mul(R, R), PPP), add(Q, Q));
+    r.y = sub(mul(sub(Q, r.x), R), mul(p1.y, PPP));
+    r.zz = mul(p1.zz, PP);
+    r.zzz = mul(p1.zzz, PPP);
+  } else if (is_zero(R)) {
+    r = xyzz_dbl_aff(p2.x, p2.y);
+    if (subtract) r.zzz = neg(r.zzz);
+  } else {
+    r = Xyzz<F>{p1.x, p1.y, fzero(F()), fzero(F())};
+  }
+  return r;
+}
+// p1 + p2   (ref ec_ops.h:642-702, add-2008-s / dbl-2008-s-1)
+template <class F>
+Xyzz<F> xyzz_add(const Xyzz<F> &p1, const Xyzz<F> &p2) {
+  if (xyzz_is_inf(p2)) return p1;
+  if (xyzz_is_inf(p1)) return p2;
+  F U1 = mul(p1.x, p2.zz), S1 = mul(p1.y, p2.zzz);
+  F P = sub(mul(p2.x, p1.zz), U1), R = sub(mul(p2.y, p1.zzz), S1);
+  Xyzz<F> r;
+  if (!is_zero(P)) {
+    F PP = mul(P, P), PPP = mul(PP, P), Q = mul(U1, PP);
+    r.x = sub(sub(mul(R, R), PPP), add(Q, Q));
+    r.y = sub(mul(sub(Q, r.x), R), mul(S1, PPP));
+    r.zz = mul(mul(p1.zz, p2.zz), PP);
+    r.zzz = mul(mul(p1.zzz, p2.zzz), PPP);
+  } else if (is_zero(R)) {  // p1 == p2: dbl-2008-s-1
+    F U = add(p1.y, p1.y), V = mul(U, U), W = mul(U, V), S = mul(p1.x, V);
+    F M = mul(p1.x, p1.x);
+    M = add(add(M, M), M);
+    r.x = sub(sub(mul(M, M), S), S);
+    r.y = sub(mul(sub(S, r.x), M), mul(W, p1.y));
+    r.zz = mul(V, p1.zz);
+    r.zzz = mul(W, p1.zzz);
+  } else {
+    r = Xyzz<F>{p1.x, p1.y, fzero(F()), fzero(F())};
+  }
+  return r;
+}
+template <class F>
+Jac<F> xyzz_to_jac(const Xyzz<F> &a) {  // ref ec_ops.h:771-777
+  return Jac<F>{mul(a.x, a.zz), mul(a.y, a.zzz), a.zz};
+}
+template <class F>
+Xyzz<F> jac_to_xyzz(const Jac<F> &a) {  // ref ec_ops.h:779-785
+  F zz = mul(a.z, a.z);
+  return Xyzz<F>{a.x, a.y, mul(zz, a.z), zz};
+}
+
 inline void be48(uint8_t out[48], const Fp &n) {
   for (int i = 0; i < 48; ++i) out[i] = (uint8_t)(n.l[(47 - i) / 8] >> (8 * ((47 - i) % 8)));
 }
