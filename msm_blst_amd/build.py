@@ -15,6 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "libmsm_mi355x.so")
+BIN = os.path.join(HERE, "bin")
 REPO = os.path.dirname(HERE)
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("MSM_OFFLOAD_ARCH", "gfx950")
@@ -66,6 +67,15 @@ def build(verbose=False, jobs=5):
         list(ex.map(run, jobs_list))
     if jobs_list or _stale(LIB, objs):
         run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", LIB] + objs)
+    # the reference-driver executables (ref main_p1.cpp / main_p2.cpp), host C++ on the C ABI
+    drv = os.path.join(HERE, "driver", "ches_driver.cpp")
+    hdr = os.path.join(REPO, "include", "msm_ches_driver.hpp")
+    for g in (1, 2):
+        exe = os.path.join(BIN, f"msm_driver_p{g}")
+        if _stale(exe, [drv, hdr, LIB]):
+            os.makedirs(BIN, exist_ok=True)
+            run(["g++", "-O2", "-std=c++17", "-Wall", f"-DMSM_DRIVER_GROUP={g}", f"-I{os.path.join(REPO, 'include')}",
+                 drv, "-o", exe, f"-L{HERE}", "-l:libmsm_mi355x.so", "-Wl,-rpath,$ORIGIN/.."])
     return LIB
 
 
