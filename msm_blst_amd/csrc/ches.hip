@@ -303,12 +303,19 @@ template <int G>
 Ches<G>::~Ches() {
   for (auto &e : ev_) (void)hipEventDestroy(e);
   for (auto &e : acc_ev_) (void)hipEventDestroy(e);
+  for (auto &e : bev_) (void)hipEventDestroy(e);
   for (int k = 0; k < 2; ++k) {
     if (ev_head_[k]) (void)hipEventDestroy(ev_head_[k]);
     if (ev_tail_[k]) (void)hipEventDestroy(ev_tail_[k]);
     if (host_out_[k]) (void)hipHostFree(host_out_[k]);
   }
-  if (tail_) (void)hipStreamDestroy(tail_);
+  for (int k = 0; k < 2; ++k) {
+    if (ev_front_[k]) (void)hipEventDestroy(ev_front_[k]);
+    if (ev_acc_[k]) (void)hipEventDestroy(ev_acc_[k]);
+  }
+  for (int k = 0; k < 2; ++k)
+    if (tails_[k]) (void)hipStreamDestroy(tails_[k]);
+  if (fstream_) (void)hipStreamDestroy(fstream_);
 }
 
 // bucket space = B plus (copies_ - 1) copies of the small buckets 1..small_;
@@ -406,20 +413,18 @@ void Ches<G>::get_table(void *out, size_t first, size_t count, hipStream_t s) {
 }
 
 template <int G>
-void Ches<G>::front(hipStream_t s, const uint8_t *d_scalars, size_t stride, hipEvent_t acc0, hipEvent_t acc1) {
-  typedef typename FieldOf<G>::F F;
+void Ches<G>::digits_sort(hipStream_t s, const uint8_t *d_scalars, size_t stride, int set) {
   const size_t n = n_, h = (size_t)p_.h, ne = n * h, NB = bucket_count();
-  keys_.ensure(ne * 4);
-  vals_.ensure(ne * 4);
-  sorted_.ensure(ne * 4);
-  counts_.ensure(NB * 4);
-  offsets_.ensure(NB * 4);
-  order_.ensure(NB * 4);
-  buckets_.ensure(NB * sizeof(Xyzz<F>));
-  if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[0], s));
+  ChesFrontSet &f = fs_[set];
+  f.keys.ensure(ne * 4);
+  f.vals.ensure(ne * 4);
+  f.sorted.ensure(ne * 4);
+  f.counts.ensure(NB * 4);
+  f.offsets.ensure(NB * 4);
+  f.order.ensure(NB * 4);
 #define MSM_CHES_DIGITS(HT)                                                                                   \
   hipLaunchKernelGGL(k_ches_digits<HT>, dim3(nblk(n, 256)), dim3(256), 0, s, d_scalars, stride, n, p_.q_exp, p_.h, \
-                     hash_.as<uint32_t>(), keys_.as<uint32_t>(), vals_.as<uint32_t>(), (uint32_t)B_.size(),      \
+                     hash_.as<uint32_t>(), f.keys.as<uint32_t>(), f.vals.as<uint32_t>(), (uint32_t)B_.size(),  \
                      (uint32_t)small_, (uint32_t)copies_)
   switch (p_.h) {  // the h of the reference configurations (ches_config_files)
     case 12: MSM_CHES_DIGITS(12); break;
@@ -433,16 +438,20 @@ void Ches<G>::front(hipStream_t s, const uint8_t *d_scalars, size_t stride, hipE
 #undef MSM_CHES_DIGITS
   MSM_HIP_CHECK(hipGetLastError());
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[1], s));
-  sort_.run(s, keys_.as<uint32_t>(), vals_.as<uint32_t>(), ne, (uint32_t)NB, sorted_.as<uint32_t>(),
-            counts_.as<uint32_t>(), offsets_.as<uint32_t>(), order_.as<uint32_t>());
-  if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[2], s));
-  if (acc0) MSM_HIP_CHECK(hipEventRecord(acc0, s));
-  hipLaunchKernelGGL((k_accumulate<G, AffP<F>>), dim3(nblk(NB, 256)), dim3(256), 0, s, order_.as<uint32_t>(),
-                     counts_.as<uint32_t>(), offsets_.as<uint32_t>(), sorted_.as<uint32_t>(), table_.as<AffP<F>>(),
-                     buckets_.as<Xyzz<F>>(), NB);
+  f.sort.run(s, f.keys.as<uint32_t>(), f.vals.as<uint32_t>(), ne, (uint32_t)NB, f.sorted.as<uint32_t>(),
+             f.counts.as<uint32_t>(), f.offsets.as<uint32_t>(), f.order.as<uint32_t>());
+}
+
+template <int G>
+void Ches<G>::accumulate(hipStream_t s, int set, int bset) {
+  typedef typename FieldOf<G>::F F;
+  const size_t NB = bucket_count();
+  ChesFrontSet &f = fs_[set];
+  buckets_[bset].ensure(NB * sizeof(Xyzz<F>));
+  hipLaunchKernelGGL((k_accumulate<G, AffP<F>>), dim3(nblk(NB, 256)), dim3(256), 0, s, f.order.as<uint32_t>(),
+                     f.counts.as<uint32_t>(), f.offsets.as<uint32_t>(), f.sorted.as<uint32_t>(), table_.as<AffP<F>>(),
+                     buckets_[bset].as<Xyzz<F>>(), NB);
   MSM_HIP_CHECK(hipGetLastError());
-  if (acc1) MSM_HIP_CHECK(hipEventRecord(acc1, s));
-  if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[3], s));
 }
 
 template <int G>
@@ -453,8 +462,12 @@ void Ches<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, hfp::J
     std::memset(out, 0, sizeof(*out));
     return;
   }
-  front(s, d_scalars, stride);
-  red_.launch(s, buckets_.p);
+  if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[0], s));
+  digits_sort(s, d_scalars, stride, 0);
+  if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[2], s));
+  accumulate(s, 0, 0);
+  if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[3], s));
+  red_.launch(s, buckets_[0].p);
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[4], s));
   *out = red_.read(s);
   if (profile_) {
@@ -487,13 +500,28 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *d_scalars, size_t stride, 
     std::memset(outs, 0, sizeof(*outs) * count);
     return;
   }
-  if (!tail_) {
-    MSM_HIP_CHECK(hipStreamCreateWithFlags(&tail_, hipStreamNonBlocking));
+  if (!fstream_) {
+    // the short digit/sort and latency-bound reduction kernels go ahead of the
+    // long accumulation's pending workgroups: highest stream priority
+    int least = 0, greatest = 0;
+    MSM_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    for (int k = 0; k < 2; ++k) MSM_HIP_CHECK(hipStreamCreateWithPriority(&tails_[k], hipStreamNonBlocking, greatest));
+    MSM_HIP_CHECK(hipStreamCreateWithPriority(&fstream_, hipStreamNonBlocking, greatest));
     for (int k = 0; k < 2; ++k) {
       MSM_HIP_CHECK(hipEventCreateWithFlags(&ev_head_[k], hipEventDisableTiming));
       MSM_HIP_CHECK(hipEventCreateWithFlags(&ev_tail_[k], hipEventDisableTiming));
-      MSM_HIP_CHECK(hipHostMalloc(&host_out_[k], red_.out_bytes() + 64, hipHostMallocDefault));
+      MSM_HIP_CHECK(hipEventCreateWithFlags(&ev_front_[k], hipEventDisableTiming));
+      MSM_HIP_CHECK(hipEventCreateWithFlags(&ev_acc_[k], hipEventDisableTiming));
     }
+  }
+  // one pinned read-back slot per MSM of the batch: the host never waits inside
+  // the issue loop, so MSM k+1's front is queued while MSM k still accumulates
+  const size_t ob = (red_.out_bytes() + 255) & ~(size_t)255;
+  if (host_out_bytes_ < count * ob) {
+    if (host_out_[0]) (void)hipHostFree(host_out_[0]);
+    host_out_[0] = nullptr;
+    MSM_HIP_CHECK(hipHostMalloc(&host_out_[0], count * ob, hipHostMallocDefault));
+    host_out_bytes_ = count * ob;
   }
   const bool prof = profile_;
   profile_ = false;
@@ -503,29 +531,46 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *d_scalars, size_t stride, 
       MSM_HIP_CHECK(hipEventCreate(&e));
       acc_ev_.push_back(e);
     }
-  // MSM k: front + level 0 on s; tail on tail_ (buffer set k & 1), then the host
-  // combines MSM k - 1 while the GPU runs MSM k.
-  for (size_t k = 0; k <= count; ++k) {
-    if (k < count) {
-      const int set = (int)(k & 1);
-      front(s, d_scalars + k * set_stride, stride, prof ? acc_ev_[2 * k] : nullptr, prof ? acc_ev_[2 * k + 1] : nullptr);
-      if (k >= 2) MSM_HIP_CHECK(hipStreamWaitEvent(s, ev_tail_[set], 0));  // set's buffers free again
-      red_.launch_head(s, buckets_.p, set);
-      MSM_HIP_CHECK(hipEventRecord(ev_head_[set], s));
-      MSM_HIP_CHECK(hipStreamWaitEvent(tail_, ev_head_[set], 0));
-      red_.launch_tail(tail_, set);
-      red_.copy_out(tail_, set, host_out_[set]);
-      MSM_HIP_CHECK(hipEventRecord(ev_tail_[set], tail_));
-    }
-    if (k >= 1) {
-      const int pset = (int)((k - 1) & 1);
-      MSM_HIP_CHECK(hipEventSynchronize(ev_tail_[pset]));
-      outs[k - 1] = red_.combine(host_out_[pset])[0];
-    }
+  // Four streams, two buffer sets (set = k & 1):
+  //   fstream_:  digits + sort of MSM k into front set k&1 (after MSM k-2's
+  //              accumulation released it) -- overlaps MSM k-1's accumulation;
+  //   s:         accumulation k into bucket set k&1 (after MSM k-2's reduction
+  //              head released it) -- back to back, the VALU-bound critical path;
+  //   tails_[set]: the whole reduction of MSM k (level 0, latency-bound tail,
+  //              read-back) beside the next accumulations.
+  // No host waits inside the loop: every MSM has its own pinned read-back slot.
+  // per-MSM events (never re-recorded inside one batch)
+  while (bev_.size() < 3 * count + 1) {
+    hipEvent_t e;
+    MSM_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    bev_.push_back(e);
   }
-  // the caller's stream observes completion of every tail
-  MSM_HIP_CHECK(hipEventRecord(ev_tail_[0], tail_));
-  MSM_HIP_CHECK(hipStreamWaitEvent(s, ev_tail_[0], 0));
+  hipEvent_t *evf = bev_.data() + 1, *eva = evf + count, *evh = eva + count;  // front, acc, head of MSM k
+  MSM_HIP_CHECK(hipEventRecord(bev_[0], s));  // the batch starts after prior work on s
+  MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, bev_[0], 0));
+  for (size_t k = 0; k < count; ++k) {
+    const int set = (int)(k & 1);
+    if (k >= 2) MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, eva[k - 2], 0));  // front set free again
+    digits_sort(fstream_, d_scalars + k * set_stride, stride, set);
+    MSM_HIP_CHECK(hipEventRecord(evf[k], fstream_));
+    MSM_HIP_CHECK(hipStreamWaitEvent(s, evf[k], 0));
+    if (k >= 2) MSM_HIP_CHECK(hipStreamWaitEvent(s, evh[k - 2], 0));  // bucket set free again
+    if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k], s));
+    accumulate(s, set, set);
+    if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k + 1], s));
+    MSM_HIP_CHECK(hipEventRecord(eva[k], s));
+    MSM_HIP_CHECK(hipStreamWaitEvent(tails_[set], eva[k], 0));
+    red_.launch_head(tails_[set], buckets_[set].p, set);
+    MSM_HIP_CHECK(hipEventRecord(evh[k], tails_[set]));
+    red_.launch_tail(tails_[set], set);
+    red_.copy_out(tails_[set], set, (uint8_t *)host_out_[0] + k * ob);
+  }
+  for (int t = 0; t < 2; ++t) {  // the caller's stream observes completion of every reduction
+    MSM_HIP_CHECK(hipEventRecord(ev_tail_[t], tails_[t]));
+    MSM_HIP_CHECK(hipStreamWaitEvent(s, ev_tail_[t], 0));
+  }
+  for (int t = 0; t < 2; ++t) MSM_HIP_CHECK(hipStreamSynchronize(tails_[t]));
+  for (size_t k = 0; k < count; ++k) outs[k] = red_.combine((const uint8_t *)host_out_[0] + k * ob)[0];
   profile_ = prof;
   if (prof) {  // average accumulation time over the batch (HIP events on stream s)
     float sum = 0;

@@ -191,6 +191,12 @@ class Pippenger {
   std::vector<hipEvent_t> ev_;
 };
 
+// digit/sort outputs of one CHES MSM (entries sorted by bucket + schedule)
+struct ChesFrontSet {
+  DevBuf keys, vals, sorted, counts, offsets, order;
+  BucketSort sort;
+};
+
 template <int G>
 class Ches {
  public:
@@ -228,16 +234,21 @@ class Ches {
   void plan_buckets(size_t n);
   bool profile_ = false;
   PhaseTimes times_;
-  DevBuf hash_, table_, keys_, vals_, counts_, offsets_, sorted_, order_, buckets_;
-  BucketSort sort_;
+  DevBuf hash_, table_, buckets_[2];  // buckets double-buffered: MSM k's reduction reads set k&1
+  // digit/sort outputs, double-buffered so that MSM k+1's digits and sort
+  // (memory/LDS-bound) run beside MSM k's accumulation (VALU-bound) in a batch
+  ChesFrontSet fs_[2];
   WeightedReducer<G> red_;
   std::vector<hipEvent_t> ev_;
-  hipStream_t tail_ = nullptr;
+  hipStream_t tails_[2] = {nullptr, nullptr}, fstream_ = nullptr;
   hipEvent_t ev_head_[2] = {nullptr, nullptr}, ev_tail_[2] = {nullptr, nullptr};
+  hipEvent_t ev_front_[2] = {nullptr, nullptr}, ev_acc_[2] = {nullptr, nullptr};
   void *host_out_[2] = {nullptr, nullptr};
+  size_t host_out_bytes_ = 0;
+  std::vector<hipEvent_t> bev_;     // batch dependency events, one per (MSM, stage)
   std::vector<hipEvent_t> acc_ev_;  // batch profiling: events around each accumulation
-  void front(hipStream_t s, const uint8_t *d_scalars, size_t stride, hipEvent_t acc0 = nullptr,
-             hipEvent_t acc1 = nullptr);  // digits, sort, accumulate
+  void digits_sort(hipStream_t s, const uint8_t *d_scalars, size_t stride, int set);
+  void accumulate(hipStream_t s, int set, int bset);
 };
 
 // BGMW95 fixed-base variant (ref main_p1.cpp:94-122, 294-398;
