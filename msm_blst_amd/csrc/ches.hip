@@ -20,6 +20,7 @@
 #include <cstring>
 
 #include "ches_kernels.hpp"
+#include "coop.hpp"
 #include "engine.hpp"
 
 #ifndef MSM_GROUP
@@ -103,7 +104,7 @@ std::vector<uint32_t> ches_digit_hash(const std::vector<int> &B, int q) {
 
 // -------------------------------------------------------------- scan reduce --
 template <int G>
-void ScanReducer<G>::launch(hipStream_t s, const void *Abuf, int W, int S) {
+void ScanReducer<G>::launch(hipStream_t s, const void *Abuf, int W, int S, bool coop) {
   typedef typename FieldOf<G>::F F;
   if (S < 1 || (S & (S - 1))) throw std::runtime_error("ScanReducer: S must be a power of two");
   const size_t NT = (size_t)W * S;
@@ -114,14 +115,16 @@ void ScanReducer<G>::launch(hipStream_t s, const void *Abuf, int W, int S) {
   int cur = 0;
   for (int d = 1; d < S; d <<= 1) {  // suffix sums T_k = sum_{b >= k} A_b
     Xyzz<F> *dst = buf[cur].as<Xyzz<F>>();
-    hipLaunchKernelGGL(k_suffix_step<G>, dim3(nblk(NT, 64)), dim3(64), 0, s, src, dst, S, d, W);
+    if (coop) hipLaunchKernelGGL(k_suffix_step_c<G>, dim3(nblk(NT, 64)), dim3(256), 0, s, src, dst, S, d, W);
+    else hipLaunchKernelGGL(k_suffix_step<G>, dim3(nblk(NT, 64)), dim3(64), 0, s, src, dst, S, d, W);
     MSM_HIP_CHECK(hipGetLastError());
     src = dst;
     cur ^= 1;
   }
   for (size_t len = NT; len > (size_t)W; len >>= 1) {  // sum_k T_k = sum_b b A_b
     Xyzz<F> *dst = buf[cur].as<Xyzz<F>>();
-    hipLaunchKernelGGL(k_pair_step<G>, dim3(nblk(len / 2, 64)), dim3(64), 0, s, src, dst, len / 2);
+    if (coop) hipLaunchKernelGGL(k_pair_step_c<G>, dim3(nblk(len / 2, 64)), dim3(256), 0, s, src, dst, len / 2);
+    else hipLaunchKernelGGL(k_pair_step<G>, dim3(nblk(len / 2, 64)), dim3(64), 0, s, src, dst, len / 2);
     MSM_HIP_CHECK(hipGetLastError());
     src = dst;
     cur ^= 1;
@@ -240,7 +243,7 @@ void WeightedReducer<G>::launch_head(hipStream_t s, const void *Sbuf, int set) {
 }
 
 template <int G>
-void WeightedReducer<G>::launch_tail(hipStream_t s, int set) {
+void WeightedReducer<G>::launch_tail(hipStream_t s, int set, bool coop) {
   typedef typename FieldOf<G>::F F;
   const size_t L = nout_.size();
   const Xyzz<F> *src = part_[set][0].as<Xyzz<F>>();
@@ -249,12 +252,16 @@ void WeightedReducer<G>::launch_tail(hipStream_t s, int set) {
     Xyzz<F> *dst = last ? dense_buf_[set].as<Xyzz<F>>() : part_[set][l & 1].as<Xyzz<F>>();
     const uint32_t *ix = last ? idx_.as<uint32_t>() + final_perm_off_ : nullptr;
     if (nout_[l])
-      hipLaunchKernelGGL(k_segsum<G>, dim3(nblk(nout_[l], 64)), dim3(64), 0, s, src, ix, starts_[l].as<uint32_t>(),
-                         dst, nout_[l]);
+      if (coop && nout_[l] <= 16384)  // few outputs: latency-bound, 4 waves per add
+        hipLaunchKernelGGL(k_segsum_c<G>, dim3(nblk(nout_[l], 64)), dim3(256), 0, s, src, ix,
+                           starts_[l].as<uint32_t>(), dst, nout_[l]);
+      else
+        hipLaunchKernelGGL(k_segsum<G>, dim3(nblk(nout_[l], 64)), dim3(64), 0, s, src, ix, starts_[l].as<uint32_t>(),
+                           dst, nout_[l]);
     MSM_HIP_CHECK(hipGetLastError());
     src = dst;
   }
-  dense_[set].launch(s, dense_buf_[set].p, 2 * nwin_, 1 << sbits_);
+  dense_[set].launch(s, dense_buf_[set].p, 2 * nwin_, 1 << sbits_, coop);
 }
 
 template <int G>
@@ -562,7 +569,7 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *d_scalars, size_t stride, 
     MSM_HIP_CHECK(hipStreamWaitEvent(tails_[set], eva[k], 0));
     red_.launch_head(tails_[set], buckets_[set].p, set);
     MSM_HIP_CHECK(hipEventRecord(evh[k], tails_[set]));
-    red_.launch_tail(tails_[set], set);
+    red_.launch_tail(tails_[set], set, false);  // beside the accumulations: least resource time
     red_.copy_out(tails_[set], set, (uint8_t *)host_out_[0] + k * ob);
   }
   for (int t = 0; t < 2; ++t) {  // the caller's stream observes completion of every reduction

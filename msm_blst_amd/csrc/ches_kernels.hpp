@@ -393,6 +393,8 @@ static __global__ void __launch_bounds__(64)
   st16(&out[t], a);
 }
 
+// 4-waves-per-add forms of the tail steps (latency): coop.hpp
+
 // blst xyzz {x, y, zzz, zz} (Montgomery R=2^384) -> internal xyzz
 template <int G>
 __global__ void k_import_xyzz(const uint64_t *__restrict__ in, Xyzz<typename FieldOf<G>::F> *__restrict__ out,

@@ -120,8 +120,10 @@ template <int G>
 struct ScanReducer {
   typedef typename HostField<G>::F HF;
   DevBuf buf[2], fin;
-  // enqueue: fin <- W blst Jacobians (144 G bytes each)
-  void launch(hipStream_t s, const void *A, int W, int S);
+  // enqueue: fin <- W blst Jacobians (144 G bytes each).  coop: one add per 4
+  // waves (coop.hpp; shortest latency when the GPU is otherwise idle) instead of
+  // one add per lane (least resource time beside other kernels)
+  void launch(hipStream_t s, const void *A, int W, int S, bool coop = true);
   void read(hipStream_t s, int W, std::vector<hfp::Jac<HF>> &out);
 };
 
@@ -141,7 +143,8 @@ class WeightedReducer {
   void plan(const std::vector<uint32_t> &w, const std::vector<uint32_t> &win, int nwin);
   void plan(const std::vector<uint32_t> &w) { plan(w, {}, 1); }
   void launch_head(hipStream_t s, const void *S, int set);  // level 0 (reads S = xyzz[w.size()])
-  void launch_tail(hipStream_t s, int set);                  // levels >= 1, dense, finalize
+  // levels >= 1, dense, finalize; coop: see ScanReducer::launch
+  void launch_tail(hipStream_t s, int set, bool coop = true);
   void launch(hipStream_t s, const void *S) {
     launch_head(s, S, 0);
     launch_tail(s, 0);
