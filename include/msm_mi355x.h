@@ -139,6 +139,14 @@ void blst_p2_tile_pippenger_BGMW95(blst_p2 *ret, const blst_p2_affine *const poi
                                    const int scalars[], const unsigned char booth_signs[], blst_p2xyzz buckets[],
                                    size_t q_exponent);
 
+/* ---- sum of affine points (replaces ref src/bulk_addition.c:145-164, blst.h:224-225) ----
+ * ret = sum of npoints affine points (all-zero = infinity).  Pointer rule of
+ * bulk_addition.c:155: a NULL entry means "the point right after the previous one"
+ * ({ptr, NULL} = one flat array).  On the GPU: entries spread over buckets of
+ * weight 1, one lane per bucket, then the bucket reduction. */
+void blst_p1s_add(blst_p1 *ret, const blst_p1_affine *const points[], size_t npoints);
+void blst_p2s_add(blst_p2 *ret, const blst_p2_affine *const points[], size_t npoints);
+
 /* ---- extension API: device-resident contexts (points uploaded once) ---- */
 enum {
   MSM_OK = 0,
@@ -199,6 +207,10 @@ int msm_ches_ctx_mult(msm_ches_ctx *ctx, void *ret, const byte *scalars, size_t 
  * of msm_ches_ctx_mult. */
 int msm_ches_ctx_mult_batch(msm_ches_ctx *ctx, void *rets, const byte *scalars, size_t stride, size_t set_stride,
                             size_t count, int scalars_on_device, void *hip_stream);
+/* table file cache (the reference rebuilds its tables on every run, main_p1.cpp:128-178):
+ * 64-byte header + the rows in blst affine layout; load checks group/method/q/h */
+int msm_ches_ctx_save_table(msm_ches_ctx *ctx, const char *path);
+int msm_ches_ctx_load_table(msm_ches_ctx *ctx, const char *path);
 int msm_ches_ctx_set_profiling(msm_ches_ctx *ctx, int on);
 int msm_ches_ctx_phase_times(const msm_ches_ctx *ctx, float out[6]);
 size_t msm_ches_ctx_bucket_count(const msm_ches_ctx *ctx);
@@ -221,6 +233,8 @@ int msm_bgmw_ctx_set_table(msm_bgmw_ctx *ctx, const void *table_affine, size_t n
 int msm_bgmw_ctx_get_table(msm_bgmw_ctx *ctx, void *out_affine, size_t first, size_t count);
 int msm_bgmw_ctx_mult(msm_bgmw_ctx *ctx, void *ret, const byte *scalars, size_t stride, int scalars_on_device,
                       void *hip_stream);
+int msm_bgmw_ctx_save_table(msm_bgmw_ctx *ctx, const char *path);
+int msm_bgmw_ctx_load_table(msm_bgmw_ctx *ctx, const char *path);
 int msm_bgmw_ctx_set_profiling(msm_bgmw_ctx *ctx, int on);
 int msm_bgmw_ctx_phase_times(const msm_bgmw_ctx *ctx, float out[6]);
 size_t msm_bgmw_ctx_bucket_count(const msm_bgmw_ctx *ctx);

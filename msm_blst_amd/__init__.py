@@ -17,7 +17,7 @@ from ._ffi import MsmError, check, lib
 from .bgmw import BGMWContext
 from .ches import CHESContext
 
-__all__ = ["MsmError", "MSMContext", "CHESContext", "BGMWContext", "p1s_mult_pippenger", "p2s_mult_pippenger", "fixed_points", "gen_scalars",
+__all__ = ["MsmError", "MSMContext", "CHESContext", "BGMWContext", "p1s_mult_pippenger", "p2s_mult_pippenger", "ps_add", "fixed_points", "gen_scalars",
            "compress", "to_affine", "device_count", "lib"]
 
 POINT_BYTES = {1: 96, 2: 192}
@@ -78,6 +78,15 @@ def p1s_mult_pippenger(points, scalars, n, nbits=255):
 
 def p2s_mult_pippenger(points, scalars, n, nbits=255):
     return _mult(2, points, scalars, n, nbits)
+
+
+def ps_add(group, points, n):
+    """Sum of n affine points (blst_p1s_add / blst_p2s_add, ref bulk_addition.c:145-164), flat array."""
+    pts = _buf(points)
+    pp = (ctypes.c_void_p * 2)(ctypes.cast(pts, ctypes.c_void_p), None)
+    ret = (ctypes.c_uint8 * JAC_BYTES[group])()
+    getattr(lib(), f"blst_p{group}s_add")(ret, pp, n)
+    return bytes(ret)
 
 
 class MSMContext:

@@ -81,6 +81,13 @@ def lib():
     L.msm_bgmw_ctx_bucket_count.restype = sz
     L.msm_bgmw_ctx_destroy.argtypes = [vp]
     L.msm_bgmw_ctx_destroy.restype = None
+    cp = ctypes.c_char_p
+    for f in ("msm_ches_ctx_save_table", "msm_ches_ctx_load_table", "msm_bgmw_ctx_save_table",
+              "msm_bgmw_ctx_load_table"):
+        getattr(L, f).argtypes = [vp, cp]
+    for g in (1, 2):
+        getattr(L, f"blst_p{g}s_add").argtypes = [vp, vp, sz]
+        getattr(L, f"blst_p{g}s_add").restype = None
     _lib = L
     return L
 

@@ -46,6 +46,21 @@ class BGMWContext:
         check(lib().msm_bgmw_ctx_get_table(self._ctx, out, first, count))
         return out
 
+    def save_table(self, path):
+        """Write the table to a file (64-B header + blst affine rows)."""
+        check(lib().msm_bgmw_ctx_save_table(self._ctx, str(path).encode()))
+
+    def load_table(self, path):
+        """Load a table written by save_table for the same group and parameters."""
+        check(lib().msm_bgmw_ctx_load_table(self._ctx, str(path).encode()))
+        self.n = self._npoints_from_file(path)
+
+    @staticmethod
+    def _npoints_from_file(path):
+        import struct
+        with open(path, "rb") as f:
+            return struct.unpack("<8s4iQQ24x", f.read(64))[5]
+
     def mult(self, scalars, stride=32, on_device=False, stream=None):
         ret = (ctypes.c_uint8 * JAC_BYTES[self.group])()
         ptr = scalars if on_device else _buf(scalars)

@@ -227,6 +227,26 @@ void tile_bgmw95(void *ret, const void *const *points, size_t n, const int *scal
   if (buckets) memset(buckets, 0, (nb + 1) * 192 * G);
 }
 
+// sum_i P_i on the GPU: entries spread over up to 4096 buckets of weight 1
+// (one lane accumulates each bucket), then the weighted reduction sums them
+template <int G>
+void points_add(void *ret, const void *const *points, size_t n) {
+  const size_t psz = 96 * G;
+  std::vector<uint8_t> flat(n * psz);
+  const uint8_t *pt = nullptr;
+  for (size_t i = 0; i < n; ++i) {
+    pt = *points ? (const uint8_t *)*points++ : pt + psz;
+    memcpy(flat.data() + i * psz, pt, psz);
+  }
+  const size_t nb = std::max<size_t>(1, std::min<size_t>(n, 4096));
+  std::vector<uint32_t> keys(n), vals(n), w(nb, 1);
+  for (size_t i = 0; i < n; ++i) {
+    keys[i] = (uint32_t)(i % nb);
+    vals[i] = (uint32_t)i;
+  }
+  entry_msm<G>(ret, flat.data(), n, keys.data(), vals.data(), n, nb, w.data(), nullptr);
+}
+
 size_t blst_window(size_t n) {  // ref multi_scalar.c:268-275
   size_t w = 0;
   while (n >>= 1) ++w;
@@ -267,6 +287,70 @@ struct msm_ctx {
   std::unique_ptr<Pippenger<2>> g2;
   DevBuf scalars;
 };
+
+namespace {
+// ---------------- table file cache ----------------
+// file = 64-byte header + rows in blst affine layout (canonical Montgomery,
+// byte-identical to the reference's PRECOMPUTATION_POINTS_LIST_3nh / _BGMW95)
+struct TableFileHeader {
+  char magic[8];  // "MSMTBL01"
+  int32_t group, method, q_exp, h;  // method: 1 CHES (3 rows per digit), 2 BGMW95 (1 row)
+  uint64_t npoints, rows;
+  uint8_t pad[24];
+};
+static_assert(sizeof(TableFileHeader) == 64, "header");
+static const size_t kTableChunk = (size_t)1 << 20;  // rows per I/O chunk
+
+template <class E>
+static int save_table_file(E &eng, int group, int method, int q_exp, int h, const char *path) {
+  FILE *f = fopen(path, "wb");
+  if (!f) return fail(MSM_E_ARG, std::string("cannot open ") + path);
+  TableFileHeader hd;
+  memset(&hd, 0, sizeof hd);
+  memcpy(hd.magic, "MSMTBL01", 8);
+  hd.group = group, hd.method = method, hd.q_exp = q_exp, hd.h = h;
+  hd.npoints = eng.npoints(), hd.rows = eng.table_rows();
+  bool ok = fwrite(&hd, sizeof hd, 1, f) == 1;
+  std::vector<uint8_t> buf(std::min<size_t>(kTableChunk, std::max<size_t>(hd.rows, 1)) * 96 * group);
+  for (size_t r0 = 0; ok && r0 < hd.rows; r0 += kTableChunk) {
+    size_t cnt = std::min(kTableChunk, (size_t)hd.rows - r0);
+    eng.get_table(buf.data(), r0, cnt, (hipStream_t)0);
+    ok = fwrite(buf.data(), 96 * group, cnt, f) == cnt;
+  }
+  ok = (fclose(f) == 0) && ok;
+  return ok ? MSM_OK : fail(MSM_E_ARG, std::string("write failed: ") + path);
+}
+
+template <class E>
+static int load_table_file(E &eng, int group, int method, int q_exp, int h, const char *path) {
+  FILE *f = fopen(path, "rb");
+  if (!f) return fail(MSM_E_ARG, std::string("cannot open ") + path);
+  TableFileHeader hd;
+  if (fread(&hd, sizeof hd, 1, f) != 1 || memcmp(hd.magic, "MSMTBL01", 8) != 0) {
+    fclose(f);
+    return fail(MSM_E_ARG, "not a table file");
+  }
+  if (hd.group != group || hd.method != method || hd.q_exp != q_exp || hd.h != h) {
+    fclose(f);
+    return fail(MSM_E_ARG, "table file was written for other parameters");
+  }
+  eng.reserve_table((size_t)hd.npoints);
+  if (eng.table_rows() != hd.rows) {
+    fclose(f);
+    return fail(MSM_E_ARG, "table file row count does not match its point count");
+  }
+  std::vector<uint8_t> buf(std::min<size_t>(kTableChunk, std::max<size_t>(hd.rows, 1)) * 96 * group);
+  bool ok = true;
+  for (size_t r0 = 0; ok && r0 < hd.rows; r0 += kTableChunk) {
+    size_t cnt = std::min(kTableChunk, (size_t)hd.rows - r0);
+    ok = fread(buf.data(), 96 * group, cnt, f) == cnt;
+    if (ok) eng.put_table(buf.data(), r0, cnt, false, (hipStream_t)0);
+  }
+  fclose(f);
+  return ok ? MSM_OK : fail(MSM_E_ARG, std::string("short read: ") + path);
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -415,6 +499,21 @@ MSM_XYZZ_HELPERS(2, hfp::Fp2)
 MSM_CHES_ENTRIES(1)
 MSM_CHES_ENTRIES(2)
 #undef MSM_CHES_ENTRIES
+
+// ---- sum of affine points (replaces ref src/bulk_addition.c:145-164) ----
+// point pointer rule of bulk_addition.c:155: a NULL entry continues right after
+// the previous point
+#define MSM_POINTS_ADD(g)                                                                                         \
+  void blst_p##g##s_add(blst_p##g *ret, const blst_p##g##_affine *const points[], size_t npoints) {             \
+    try {                                                                                                         \
+      points_add<g>(ret, (const void *const *)points, npoints);                                                   \
+    } catch (const std::exception &e) {                                                                           \
+      die("blst_p" #g "s_add", e);                                                                                \
+    }                                                                                                             \
+  }
+MSM_POINTS_ADD(1)
+MSM_POINTS_ADD(2)
+#undef MSM_POINTS_ADD
 
 const char *msm_last_error(void) { return g_err.c_str(); }
 
@@ -737,6 +836,55 @@ int msm_bgmw_ctx_phase_times(const msm_bgmw_ctx *ctx, float out[6]) {
 size_t msm_bgmw_ctx_bucket_count(const msm_bgmw_ctx *ctx) { return ctx ? CHES_DISPATCH(ctx, bucket_count()) : 0; }
 
 void msm_bgmw_ctx_destroy(msm_bgmw_ctx *ctx) { delete ctx; }
+
+int msm_ches_ctx_save_table(msm_ches_ctx *ctx, const char *path) {
+  if (!ctx || !path) return fail(MSM_E_ARG, "bad args");
+  try {
+    DeviceGuard g(ctx->device);
+    if (ctx->group == 1) {
+      const ChesParams &p = ctx->g1->params();
+      return save_table_file(*ctx->g1, 1, 1, p.q_exp, p.h, path);
+    }
+    const ChesParams &p = ctx->g2->params();
+    return save_table_file(*ctx->g2, 2, 1, p.q_exp, p.h, path);
+  } catch (const std::exception &e) {
+    return fail(MSM_E_HIP, e.what());
+  }
+}
+int msm_ches_ctx_load_table(msm_ches_ctx *ctx, const char *path) {
+  if (!ctx || !path) return fail(MSM_E_ARG, "bad args");
+  try {
+    DeviceGuard g(ctx->device);
+    if (ctx->group == 1) {
+      const ChesParams &p = ctx->g1->params();
+      return load_table_file(*ctx->g1, 1, 1, p.q_exp, p.h, path);
+    }
+    const ChesParams &p = ctx->g2->params();
+    return load_table_file(*ctx->g2, 2, 1, p.q_exp, p.h, path);
+  } catch (const std::exception &e) {
+    return fail(MSM_E_HIP, e.what());
+  }
+}
+int msm_bgmw_ctx_save_table(msm_bgmw_ctx *ctx, const char *path) {
+  if (!ctx || !path) return fail(MSM_E_ARG, "bad args");
+  try {
+    DeviceGuard g(ctx->device);
+    if (ctx->group == 1) return save_table_file(*ctx->g1, 1, 2, ctx->g1->q_exp(), ctx->g1->h(), path);
+    return save_table_file(*ctx->g2, 2, 2, ctx->g2->q_exp(), ctx->g2->h(), path);
+  } catch (const std::exception &e) {
+    return fail(MSM_E_HIP, e.what());
+  }
+}
+int msm_bgmw_ctx_load_table(msm_bgmw_ctx *ctx, const char *path) {
+  if (!ctx || !path) return fail(MSM_E_ARG, "bad args");
+  try {
+    DeviceGuard g(ctx->device);
+    if (ctx->group == 1) return load_table_file(*ctx->g1, 1, 2, ctx->g1->q_exp(), ctx->g1->h(), path);
+    return load_table_file(*ctx->g2, 2, 2, ctx->g2->q_exp(), ctx->g2->h(), path);
+  } catch (const std::exception &e) {
+    return fail(MSM_E_HIP, e.what());
+  }
+}
 
 size_t msm_ches_bucket_set(int q, int a_h, int *out, size_t cap) {
   if (q < 4 || a_h < 0) return 0;

@@ -108,26 +108,39 @@ void Bgmw<G>::build_table(const void *pts, size_t n, bool on_device, hipStream_t
 }
 
 template <int G>
-void Bgmw<G>::set_table(const void *tab, size_t n, bool on_device, hipStream_t s) {
+void Bgmw<G>::reserve_table(size_t n) {
   typedef typename FieldOf<G>::F F;
   DeviceGuard g(dev_);
   const size_t cnt = (size_t)h_ * n;
-  if (cnt >= (1ull << 31)) throw std::runtime_error("BGMW95 table too large for 31-bit slots");
-  const void *src = tab;
-  DevBuf stage;
-  if (!on_device && cnt) {
-    stage.ensure(cnt * 96 * G);
-    MSM_HIP_CHECK(hipMemcpyAsync(stage.p, tab, cnt * 96 * G, hipMemcpyHostToDevice, s));
-    src = stage.p;
-  }
+  if (cnt >= (1ull << 31)) throw std::runtime_error("table too large for 31-bit slots");
   table_.ensure(std::max<size_t>(cnt, 1) * sizeof(AffP<F>));
-  if (cnt)
-    hipLaunchKernelGGL((k_convert_points<G, AffP<F>>), dim3(nblk(cnt, 256)), dim3(256), 0, s, (const uint64_t *)src,
-                       table_.as<AffP<F>>(), cnt);
-  MSM_HIP_CHECK(hipGetLastError());
-  MSM_HIP_CHECK(hipStreamSynchronize(s));
   n_ = n;
   plan_buckets(n);
+}
+
+template <int G>
+void Bgmw<G>::put_table(const void *tab, size_t first, size_t count, bool on_device, hipStream_t s) {
+  typedef typename FieldOf<G>::F F;
+  DeviceGuard g(dev_);
+  if (first + count > table_rows()) throw std::runtime_error("table rows out of range");
+  if (!count) return;
+  const void *src = tab;
+  DevBuf stage;
+  if (!on_device) {
+    stage.ensure(count * 96 * G);
+    MSM_HIP_CHECK(hipMemcpyAsync(stage.p, tab, count * 96 * G, hipMemcpyHostToDevice, s));
+    src = stage.p;
+  }
+  hipLaunchKernelGGL((k_convert_points<G, AffP<F>>), dim3(nblk(count, 256)), dim3(256), 0, s, (const uint64_t *)src,
+                     table_.as<AffP<F>>() + first, count);
+  MSM_HIP_CHECK(hipGetLastError());
+  MSM_HIP_CHECK(hipStreamSynchronize(s));
+}
+
+template <int G>
+void Bgmw<G>::set_table(const void *tab, size_t n, bool on_device, hipStream_t s) {
+  reserve_table(n);
+  put_table(tab, 0, table_rows(), on_device, s);
 }
 
 template <int G>

@@ -212,6 +212,11 @@ class Ches {
   void set_table(const void *table_blst, size_t n, bool on_device, hipStream_t s);
   // copy T[first, first+count) back in blst affine layout (host memory)
   void get_table(void *out_blst, size_t first, size_t count, hipStream_t s);
+  // chunked table upload (file cache): reserve rows for n base points, then
+  // put rows [first, first + count) from blst affine layout (host or device)
+  void reserve_table(size_t n);
+  void put_table(const void *rows_blst, size_t first, size_t count, bool on_device, hipStream_t s);
+  size_t table_rows() const { return 3 * (size_t)p_.h * n_; }
   // scalars: n 32-byte LE strings (stride >= 32) on device
   void run(hipStream_t s, const uint8_t *d_scalars, size_t stride, hfp::Jac<HF> *out);
   // `count` MSMs over the same points; scalar set k at d_scalars + k * set_stride.
@@ -267,6 +272,9 @@ class Bgmw {
   void build_table(const void *points_blst, size_t n, bool on_device, hipStream_t s);
   void set_table(const void *table_blst, size_t n, bool on_device, hipStream_t s);  // n h points
   void get_table(void *out_blst, size_t first, size_t count, hipStream_t s);
+  void reserve_table(size_t n);
+  void put_table(const void *rows_blst, size_t first, size_t count, bool on_device, hipStream_t s);
+  size_t table_rows() const { return (size_t)h_ * n_; }
   // scalars: n 32-byte LE strings (stride >= 32) on device
   void run(hipStream_t s, const uint8_t *d_scalars, size_t stride, hfp::Jac<HF> *out);
   size_t npoints() const { return n_; }
