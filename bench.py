@@ -32,6 +32,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 METRIC = "G1 MSM point-scalar pairs/sec at n=2^20, 1/2/4/8 MI355X; bit-exact vs CPU"
+METRIC_G2 = "G2 MSM point-scalar pairs/sec at n=2^20 (BASELINE configs[4]); bit-exact vs CPU"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 VALU_PEAK_LANE_OPS = 78.6e12   # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (one VALU op / lane / clk)
 MADS_PER_FPMUL = 392           # 14x14 product + 14x14 reduction, one v_mad_u64_u32 each (fp.hpp)
@@ -86,7 +87,7 @@ def timed_batch(ctx, steps, warmup, world, dev, add):
     t_start = time.perf_counter()
     parts = ctx._bench_batch(steps)
     if world > 1:
-        res = [mdist.fold(mdist.gather_partials(p, 1, dev), add) for p in parts][-1]
+        res = [mdist.fold(mdist.gather_partials(p, ctx.group, dev), add) for p in parts][-1]
     else:
         res = parts[-1]
     torch.cuda.synchronize(dev)
@@ -108,6 +109,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--log-n", type=int, default=20, help="points per GPU = 2^log_n")
     ap.add_argument("--method", choices=("ches", "pippenger", "bgmw"), default="ches")
+    ap.add_argument("--group", type=int, choices=(1, 2), default=1,
+                    help="1: G1 (the BASELINE metric); 2: G2 (configs[4], Fp2 tower), reported under its own metric")
     ap.add_argument("--window", type=int, default=16, help="plain Pippenger window bits")
     ap.add_argument("--no-compare", action="store_true", help="skip timing the other method (N = 1)")
     ap.add_argument("--no-batch", action="store_true",
@@ -140,17 +143,18 @@ def main():
     n = 1 << args.log_n
     t0 = time.time()
     start, _ = mdist.shard_range(n * world, world, rank)
-    pts = m.fixed_points(1, n, start)
+    G = args.group
+    pts = m.fixed_points(G, n, start)
     sc = m.gen_scalars(n, 1 + rank)
     log(f"[rank {rank}] inputs generated in {time.time() - t0:.1f}s (points {start}..{start + n})")
     stream = torch.cuda.current_stream(dev)
     d_sc = torch.frombuffer(bytearray(bytes(sc)), dtype=torch.uint8).to(dev)
-    add = mdist.engine_add(1)
+    add = mdist.engine_add(G)
 
     def make(method):
         t = time.time()
         if method == "ches":
-            ctx = m.CHESContext(1, local, n_exp=args.log_n)
+            ctx = m.CHESContext(G, local, n_exp=args.log_n)
             ctx.build_table(pts, n, stream=stream.cuda_stream)
 
             def mult():
@@ -161,13 +165,13 @@ def main():
                                       stream=stream.cuda_stream)
             ctx._bench_batch = mult_batch
         elif method == "bgmw":
-            ctx = m.BGMWContext(1, local, n_exp=args.log_n)
+            ctx = m.BGMWContext(G, local, n_exp=args.log_n)
             ctx.build_table(pts, n, stream=stream.cuda_stream)
 
             def mult():
                 return ctx.mult(d_sc.data_ptr(), 32, on_device=True, stream=stream.cuda_stream)
         else:
-            ctx = m.MSMContext(1, local, args.window)
+            ctx = m.MSMContext(G, local, args.window)
             ctx.set_points(pts, n, stream=stream.cuda_stream)
 
             def mult():
@@ -179,7 +183,7 @@ def main():
         def step():
             part = mult()
             if world > 1:
-                return mdist.fold(mdist.gather_partials(part, 1, dev), add)
+                return mdist.fold(mdist.gather_partials(part, G, dev), add)
             return part
         return ctx, step
 
@@ -192,16 +196,16 @@ def main():
     else:
         res, elapsed, acc_ms, tot_ms, phases = timed_steps(step, ctx, args.steps, args.warmup, world, dev)
 
-    gold = json.load(open(os.path.join(REPO, "tests", "golden", "msm_g1.json")))
+    gold = json.load(open(os.path.join(REPO, "tests", "golden", f"msm_g{G}.json")))
     want = [c["compressed"] for c in gold["cases"] if c["n"] == n and c["seed"] == 1 and c["case"] == "rand"]
-    parity = (m.compress(1, res).hex() == want[0]) if (world == 1 and want) else None
+    parity = (m.compress(G, res).hex() == want[0]) if (world == 1 and want) else None
 
     sync = None
     if batched and world == 1 and not args.no_compare:  # the same MSMs issued one by one (no overlap)
         sres, sel, _, _, sph = timed_steps(step, ctx, args.steps, 1, world, dev)
         sync = {"value": round(n * args.steps / sel, 1), "unit": "pairs/s",
                 "ms_per_step": round(sel / args.steps * 1e3, 4),
-                "parity_vs_reference": (m.compress(1, sres).hex() == want[0]) if want else None,
+                "parity_vs_reference": (m.compress(G, sres).hex() == want[0]) if want else None,
                 "note": "K synchronous msm_ches_ctx_mult calls (per-MSM latency)"}
     others = {}
     if world == 1 and not args.no_compare:  # the reference's other methods, same points and scalars
@@ -214,7 +218,7 @@ def main():
             others[ometh] = {"value": round(n * k / oel, 1), "unit": "pairs/s",
                              "ms_per_step": round(oel / k * 1e3, 4),
                              "phases_ms": {kk: round(v, 4) for kk, v in oph.items()},
-                             "parity_vs_reference": (m.compress(1, ores).hex() == want[0]) if want else None}
+                             "parity_vs_reference": (m.compress(G, ores).hex() == want[0]) if want else None}
             octx.close()
 
     if rank != 0:
@@ -227,23 +231,23 @@ def main():
     if args.method == "ches":
         h = ctx.params["h"]
         madds = n * h                                 # one table point per (i, j) digit
-        alg_bytes = n * h * AFFINE_BYTES              # h affine gathers per pair (1184 B/pair incl. scalar)
-        workload = (f"G1 MSM n=2^{args.log_n} per GPU, CHES nh+q/5 (q=2^{ctx.params['q_exp']}, h={h}, "
+        alg_bytes = n * h * AFFINE_BYTES * G              # h affine gathers per pair (1184 B/pair incl. scalar)
+        workload = (f"G{G} MSM n=2^{args.log_n} per GPU, CHES nh+q/5 (q=2^{ctx.params['q_exp']}, h={h}, "
                     f"|B|={ctx.params['b_size']}), table T=m*q^j*P_i resident in HBM, scalars resident in HBM")
         cfg_extra = {"method": "ches_q_over_5", "q_exp": ctx.params["q_exp"], "h": h,
                      "bucket_set": ctx.params["b_size"], "buckets_incl_top_digit_copies": ctx.bucket_count()}
     elif args.method == "bgmw":
         h = ctx.h
         madds = n * h
-        alg_bytes = n * h * AFFINE_BYTES
-        workload = (f"G1 MSM n=2^{args.log_n} per GPU, BGMW95 (q=2^{ctx.q_exp}, h={h}), table q^j*P_i resident in HBM, "
+        alg_bytes = n * h * AFFINE_BYTES * G
+        workload = (f"G{G} MSM n=2^{args.log_n} per GPU, BGMW95 (q=2^{ctx.q_exp}, h={h}), table q^j*P_i resident in HBM, "
                     f"scalars resident in HBM")
         cfg_extra = {"method": "bgmw95", "q_exp": ctx.q_exp, "h": h}
     else:
         W = (255 + 1 + args.window - 1) // args.window
         madds = n * W
-        alg_bytes = n * (AFFINE_BYTES + 32)
-        workload = (f"G1 MSM n=2^{args.log_n} per GPU, plain Pippenger c={args.window} ({W} windows), "
+        alg_bytes = n * (AFFINE_BYTES * G + 32)
+        workload = (f"G{G} MSM n=2^{args.log_n} per GPU, plain Pippenger c={args.window} ({W} windows), "
                     f"points+scalars resident in HBM")
         cfg_extra = {"method": "pippenger", "window_bits": args.window}
     achieved_gbs = alg_bytes / acc_s / 1e9
@@ -251,18 +255,19 @@ def main():
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            if tj.get("method") == args.method and tj.get("log_n") == args.log_n:
+            if tj.get("method") == args.method and tj.get("log_n") == args.log_n and tj.get("group", 1) == G:
                 traffic = tj.get("accumulate_bytes_per_launch")
         except Exception:
             traffic = None
-    fpmul_rate = madds * FPMUL_PER_MADD / acc_s
+    fpm_per_madd = FPMUL_PER_MADD if G == 1 else 28   # Fp2: 8M + 2S = 8*3 + 2*2 Fp-mul
+    fpmul_rate = madds * fpm_per_madd / acc_s
 
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(m, pts, sc, args.cpu_sample_log_n)
+        cpu = cpu_baseline(m, pts, sc, args.cpu_sample_log_n if G == 1 else min(args.cpu_sample_log_n, 18), G)
 
     line = {
-        "metric": METRIC,
+        "metric": METRIC if G == 1 else METRIC_G2,
         "value": round(value, 1),
         "unit": "pairs/s",
         "n_gpus": world,
@@ -272,10 +277,10 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u32 (exact Fp381 integer arithmetic, 14x28-bit limbs)",
+        "dtype": "u32 (exact Fp381 integer arithmetic, 14x28-bit limbs)" + ("" if G == 1 else ", Fp2 = Fp[i]/(i^2+1)"),
         "data": "synthetic: P_i = 2^(i+1) G1 (main_p1.cpp:52-66), SplitMix64 scalars < r (BASELINE.md sec.3)",
         "config": dict({"workload": workload, "n_per_gpu": n, "n_total": n * world,
-                        "parallelism": f"points sharded x{world}, RCCL all_gather of 144-B partials"}, **cfg_extra),
+                        "parallelism": f"points sharded x{world}, RCCL all_gather of {144 * G}-B partials"}, **cfg_extra),
         "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved_gbs / HBM_PEAK_GBS, 5), "traffic": traffic,
                      "kernel": "k_accumulate (bucket accumulation)", "kernel_ms": round(acc_s * 1e3, 4),
@@ -284,7 +289,7 @@ def main():
         "valu_roofline": {"bound": "valu-int", "achieved": round(fpmul_rate / 1e9, 2),
                           "peak": round(FPMUL_PEAK / 1e9, 2), "unit": "G Fp-mul/s",
                           "frac": round(fpmul_rate / FPMUL_PEAK, 4),
-                          "work": f"{madds} xyzz madds x {FPMUL_PER_MADD} Fp-mul",
+                          "work": f"{madds} xyzz madds x {fpm_per_madd} Fp-mul",
                           "peak_basis": "measured register-resident Fp-mul kernel (tools/microbench/fp_rate.hip)"},
         "phases_ms": {k: round(v, 4) for k, v in phases.items()},
         "phases_note": "one synchronous MSM (profiled) after the timed region" if batched else "last timed step",
@@ -301,45 +306,46 @@ def main():
         torch.distributed.destroy_process_group()
 
 
-def cpu_baseline(m, pts, sc, log_n):
-    """The reference's own blst_p1s_mult_pippenger (libblst built from /root/reference
+def cpu_baseline(m, pts, sc, log_n, G=1):
+    """The reference's own blst_p{1,2}s_mult_pippenger (libblst built from /root/reference
     sources into oracle/_ref/libblst_ref.so, x86-64 mulx asm), 1 thread -- the
     reference has no threading -- timed on this host's cores on the same points and
     scalars; falls back to the oracle port (oracle/msm_oracle.c) if the reference
     build is absent.  The result is cross-checked against the GPU result."""
     import ctypes
     k = 1 << log_n
-    P = (ctypes.c_uint8 * (96 * k)).from_buffer_copy(bytes(pts)[:96 * k])
+    P = (ctypes.c_uint8 * (96 * G * k)).from_buffer_copy(bytes(pts)[:96 * G * k])
     S = (ctypes.c_uint8 * (32 * k)).from_buffer_copy(bytes(sc)[:32 * k])
     ref_so = os.path.join(REPO, "oracle", "_ref", "libblst_ref.so")
     if os.path.exists(ref_so):
         R = ctypes.CDLL(ref_so)
-        R.blst_p1s_mult_pippenger_scratch_sizeof.restype = ctypes.c_size_t
-        R.blst_p1s_mult_pippenger_scratch_sizeof.argtypes = [ctypes.c_size_t]
-        R.blst_p1s_mult_pippenger.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_void_p, ctypes.c_size_t,
-                                                                        ctypes.c_void_p]
-        R.blst_p1s_mult_pippenger.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
-                                              ctypes.c_size_t, ctypes.c_void_p]
-        scratch = (ctypes.c_uint8 * R.blst_p1s_mult_pippenger_scratch_sizeof(k))()
+        sizeof = getattr(R, f"blst_p{G}s_mult_pippenger_scratch_sizeof")
+        sizeof.restype = ctypes.c_size_t
+        sizeof.argtypes = [ctypes.c_size_t]
+        mult = getattr(R, f"blst_p{G}s_mult_pippenger")
+        mult.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
+                         ctypes.c_void_p]
+        scratch = (ctypes.c_uint8 * sizeof(k))()
         pp = (ctypes.c_void_p * 2)(ctypes.cast(P, ctypes.c_void_p), None)
         sp = (ctypes.c_void_p * 2)(ctypes.cast(S, ctypes.c_void_p), None)
-        r = (ctypes.c_uint8 * 144)()
+        r = (ctypes.c_uint8 * (144 * G))()
         t = time.perf_counter()
-        R.blst_p1s_mult_pippenger(r, pp, k, sp, 255, scratch)
+        mult(r, pp, k, sp, 255, scratch)
         dt = time.perf_counter() - t
-        out = (ctypes.c_uint8 * 48)()
-        R.blst_p1_compress(out, r)
-        cpu_res, kind, what = bytes(out).hex(), "reference", "reference libblst blst_p1s_mult_pippenger (oracle/_ref)"
+        out = (ctypes.c_uint8 * (48 * G))()
+        getattr(R, f"blst_p{G}_compress")(out, r)
+        cpu_res, kind = bytes(out).hex(), "reference"
+        what = f"reference libblst blst_p{G}s_mult_pippenger (oracle/_ref)"
     else:
         sys.path.insert(0, os.path.join(REPO, "tests"))
         import oracle_ffi as of
         t = time.perf_counter()
-        r = of.msm(1, P, S, k, 255, "pippenger")
+        r = of.msm(G, P, S, k, 255, "pippenger")
         dt = time.perf_counter() - t
-        cpu_res, kind, what = of.compress(1, r), "port", "oracle port of blst Pippenger (oracle/msm_oracle.c)"
-    ctx = m.CHESContext(1, 0, n_exp=log_n)
+        cpu_res, kind, what = of.compress(G, r), "port", "oracle port of blst Pippenger (oracle/msm_oracle.c)"
+    ctx = m.CHESContext(G, 0, n_exp=log_n)
     ctx.build_table(P, k)
-    gpu_res = m.compress(1, ctx.mult(S)).hex()
+    gpu_res = m.compress(G, ctx.mult(S)).hex()
     ctx.close()
     return {"value": round(k / dt, 1), "unit": "pairs/s", "cores": 1, "kind": kind,
             "sample": f"{what}, 1 thread, first 2^{log_n} points/scalars of the rank-0 workload, {dt:.1f}s",

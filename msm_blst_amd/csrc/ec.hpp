@@ -89,7 +89,7 @@ __device__ __forceinline__ void xyzz_madd(Xyzz<F> &acc, const Aff<F> &p, bool ne
     xyzz_from_aff(acc, p, neg);
     return;
   }
-  F y2, P, R, PP, PPP, Q, t;
+  F y2, P, R, PP, PPP, t;
   if (neg) {
     f_neg4(y2, p.y);       // < 4p, limbs < 2^29
   } else {
@@ -113,22 +113,23 @@ __device__ __forceinline__ void xyzz_madd(Xyzz<F> &acc, const Aff<F> &p, bool ne
     }
     return;
   }
-  f_mul(PPP, PP, P);       // S
-  f_mul(Q, acc.x, PP);     // Q = X1 PP            S
-  F X3, Y3;
+  // ordered so that ZZ1, P, X1 and PP die as early as possible (register
+  // pressure: 8-10 live field elements; G2 elements are 28 VGPRs each)
+  f_mul(acc.zz, acc.zz, PP);    // ZZ3 = ZZ1 PP         S
+  f_mul(PPP, PP, P);            // S
+  f_mul(acc.x, acc.x, PP);      // Q = X1 PP  (in place of X1)   S
+  f_mul(acc.zzz, acc.zzz, PPP); // ZZZ3 = ZZZ1 PPP      S
+  F X3;
   f_sqr(X3, R);            // R^2                  S
   f_sub4(X3, X3, PPP);     // < 6p
   f_norm(X3);
-  f_sub4(X3, X3, Q);       // < 10p
+  f_sub4(X3, X3, acc.x);   // < 10p
   f_norm(X3);
-  f_sub4(X3, X3, Q);       // < 14p
+  f_sub4(X3, X3, acc.x);   // < 14p
   f_nred(X3);              // X3 = R^2 - PPP - 2Q  S
-  f_sub4(t, Q, X3);        // < 6p
-  f_mul_sub(Y3, t, R, acc.y, PPP);  // R (Q - X3) - Y1 PPP   S (one reduction)
-  f_mul(acc.zz, acc.zz, PP);
-  f_mul(acc.zzz, acc.zzz, PPP);
+  f_sub4(t, acc.x, X3);    // Q - X3  < 6p
+  f_mul_sub(acc.y, t, R, acc.y, PPP);  // Y3 = R (Q - X3) - Y1 PPP   S (one reduction)
   acc.x = X3;
-  acc.y = Y3;
 }
 
 // acc += b, both xyzz in S
