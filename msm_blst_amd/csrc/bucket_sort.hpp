@@ -25,7 +25,7 @@
 
 namespace msm {
 
-constexpr int BS_TILE = 8192;         // entries per tile (256 threads x 32)
+constexpr int BS_TILE = 4096;         // entries per tile (256 threads x 16; staged in 32 KiB of LDS)
 constexpr int BS_MAX_FB_BITS = 12;    // fine buckets per coarse bin <= 4096 (2 x 16 KiB LDS)
 constexpr int BS_MAX_CB = 8192;       // coarse bins held in LDS (32 KiB)
 constexpr uint32_t BS_NONE = 0xffffffffu;
@@ -50,16 +50,56 @@ static __global__ void __launch_bounds__(256)
   for (int b = threadIdx.x; b < ncb; b += blockDim.x) ghist[(size_t)b * ntiles + blockIdx.x] = h[b];
 }
 
+// exclusive scan of a[0..n) in LDS by a 256-thread block (n <= 256 * 32);
+// returns the total.  wsum: 4 words of LDS scratch.
+__device__ __forceinline__ uint32_t block_exclusive_scan_256(uint32_t *a, int n, uint32_t *wsum) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int per = (n + 255) / 256, lo = t * per, hi = min(n, lo + per);
+  uint32_t s = 0;
+  for (int i = lo; i < hi; ++i) s += a[i];
+  uint32_t incl = s;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t v = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += v;
+  }
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  uint32_t before = 0, total = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    before += w < wave ? wsum[w] : 0u;
+    total += wsum[w];
+  }
+  uint32_t run = before + incl - s;
+  for (int i = lo; i < hi; ++i) {
+    uint32_t x = a[i];
+    a[i] = run;
+    run += x;
+  }
+  __syncthreads();
+  return total;
+}
+
+// Per tile: rank the entries by coarse bin in LDS, stage the tile bin-sorted in
+// LDS, then stream it out so that consecutive lanes write consecutive addresses
+// of a bin's run (coalesced), instead of 64 lanes writing 64 different bins.
+// Dynamic LDS: 2 ncb + 2 BS_TILE words.
 static __global__ void __launch_bounds__(256)
     k_bs_coarse(const uint32_t *__restrict__ keys, const uint32_t *__restrict__ vals, size_t ne, int fb_bits,
                 int ncb, int ntiles, const uint32_t *__restrict__ gbase, uint32_t *__restrict__ okeys,
                 uint32_t *__restrict__ ovals) {
-  __shared__ uint32_t cur[BS_MAX_CB];
-  for (int b = threadIdx.x; b < ncb; b += blockDim.x) cur[b] = gbase[(size_t)b * ntiles + blockIdx.x];
+  extern __shared__ uint32_t sm[];
+  __shared__ uint32_t wsum[4];
+  uint32_t *loff = sm, *gb = sm + ncb, *sk = sm + 2 * ncb, *sv = sk + BS_TILE;
+  for (int b = threadIdx.x; b < ncb; b += blockDim.x) {
+    loff[b] = 0;
+    gb[b] = gbase[(size_t)b * ntiles + blockIdx.x];
+  }
   __syncthreads();
   const size_t t0 = (size_t)blockIdx.x * BS_TILE;
   constexpr int R = BS_TILE / 256;
-  uint32_t kk[R], vv[R];
+  uint32_t kk[R], vv[R], rk[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     size_t e = t0 + threadIdx.x + (size_t)r * 256;
@@ -67,11 +107,22 @@ static __global__ void __launch_bounds__(256)
     vv[r] = e < ne ? vals[e] : 0u;
   }
 #pragma unroll
+  for (int r = 0; r < R; ++r) rk[r] = kk[r] != BS_NONE ? atomicAdd(&loff[kk[r] >> fb_bits], 1u) : 0u;
+  __syncthreads();
+  const uint32_t total = block_exclusive_scan_256(loff, ncb, wsum);
+#pragma unroll
   for (int r = 0; r < R; ++r) {
     if (kk[r] == BS_NONE) continue;
-    uint32_t pos = atomicAdd(&cur[kk[r] >> fb_bits], 1u);
-    okeys[pos] = kk[r];
-    ovals[pos] = vv[r];
+    const uint32_t pos = loff[kk[r] >> fb_bits] + rk[r];
+    sk[pos] = kk[r];
+    sv[pos] = vv[r];
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < total; i += 256) {
+    const uint32_t k = sk[i], b = k >> fb_bits;
+    const uint32_t g = gb[b] + (i - loff[b]);
+    okeys[g] = k;
+    ovals[g] = sv[i];
   }
 }
 
@@ -171,18 +222,26 @@ static __global__ void __launch_bounds__(1024)
 
 // ---- accumulation schedule: bucket ids ordered by entry count, descending ----
 // class = 255 - min(count, 255).  k_sched_hist: per-class totals (LDS histogram
-// per 256 buckets, one global atomic per non-empty class).  k_sched_scatter:
-// each workgroup reserves its per-class ranges with one global atomic per class
-// and writes its bucket ids.  The order inside a class is arbitrary.
+// per SCHED_PER_BLOCK buckets, one global atomic per non-empty class and block).
+// k_sched_scatter: each workgroup reserves its per-class ranges with one global
+// atomic per class and writes its bucket ids.  The order inside a class is
+// arbitrary.  A block covers 4096 buckets so that the ~20 busy class counters
+// see a few hundred atomics, not one per 256 buckets (a single address
+// saturates at ~88 atomics/us, MI355X_MICROARCH.md).
+constexpr int SCHED_PER_THREAD = 16;
+constexpr int SCHED_PER_BLOCK = 256 * SCHED_PER_THREAD;
+__device__ __forceinline__ uint32_t sched_class(uint32_t c) { return 255u - (c < 255u ? c : 255u); }
+
 static __global__ void __launch_bounds__(256)
     k_sched_hist(const uint32_t *__restrict__ counts, uint32_t nb, uint32_t *__restrict__ class_total) {
   __shared__ uint32_t h[256];
-  const uint32_t t = threadIdx.x, b = blockIdx.x * 256 + t;
+  const uint32_t t = threadIdx.x, b0 = blockIdx.x * SCHED_PER_BLOCK;
   h[t] = 0;
   __syncthreads();
-  if (b < nb) {
-    uint32_t c = counts[b];
-    atomicAdd(&h[255u - (c < 255u ? c : 255u)], 1u);
+#pragma unroll
+  for (int r = 0; r < SCHED_PER_THREAD; ++r) {
+    const uint32_t b = b0 + r * 256 + t;
+    if (b < nb) atomicAdd(&h[sched_class(counts[b])], 1u);
   }
   __syncthreads();
   if (h[t]) atomicAdd(&class_total[t], h[t]);
@@ -209,19 +268,24 @@ static __global__ void __launch_bounds__(256)
                     uint32_t *__restrict__ order) {
   __shared__ uint32_t h[256];
   __shared__ uint32_t base[256];
-  const uint32_t t = threadIdx.x, b = blockIdx.x * 256 + t;
+  const uint32_t t = threadIdx.x, b0 = blockIdx.x * SCHED_PER_BLOCK;
   h[t] = 0;
   __syncthreads();
-  uint32_t cls = 0, rank = 0;
-  if (b < nb) {
-    uint32_t c = counts[b];
-    cls = 255u - (c < 255u ? c : 255u);
-    rank = atomicAdd(&h[cls], 1u);
+  uint32_t cls[SCHED_PER_THREAD], rank[SCHED_PER_THREAD];
+#pragma unroll
+  for (int r = 0; r < SCHED_PER_THREAD; ++r) {
+    const uint32_t b = b0 + r * 256 + t;
+    cls[r] = b < nb ? sched_class(counts[b]) : 0u;
+    rank[r] = b < nb ? atomicAdd(&h[cls[r]], 1u) : 0u;
   }
   __syncthreads();
   if (h[t]) base[t] = atomicAdd(&class_cursor[t], h[t]);
   __syncthreads();
-  if (b < nb) order[base[cls] + rank] = b;
+#pragma unroll
+  for (int r = 0; r < SCHED_PER_THREAD; ++r) {
+    const uint32_t b = b0 + r * 256 + t;
+    if (b < nb) order[base[cls[r]] + rank[r]] = b;
+  }
 }
 
 // total number of valid entries = inclusive end of the last (bin, tile) slot

@@ -24,7 +24,7 @@ void BucketSort::run(hipStream_t s, const uint32_t *keys, const uint32_t *vals, 
   int fb_bits = 8;
   while (fb_bits < BS_MAX_FB_BITS && ((size_t)nb >> fb_bits) > 384) ++fb_bits;
   const int ncb = (int)(((size_t)nb + (1u << fb_bits) - 1) >> fb_bits);
-  if (ncb > BS_MAX_CB) throw std::runtime_error("BucketSort: too many buckets");
+  if (ncb > BS_MAX_CB || ncb > 4096) throw std::runtime_error("BucketSort: too many buckets");
   if (ne >= (1ull << 32)) throw std::runtime_error("BucketSort: too many entries");
   const int ntiles = (int)std::max<size_t>(1, (ne + BS_TILE - 1) / BS_TILE);
   const size_t nslots = (size_t)ncb * ntiles;
@@ -42,17 +42,19 @@ void BucketSort::run(hipStream_t s, const uint32_t *keys, const uint32_t *vals, 
   MSM_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, ghist.as<uint32_t>(), gbase.as<uint32_t>(), (int)nslots, s));
   hipLaunchKernelGGL(k_bs_total, dim3(1), dim3(64), 0, s, gbase.as<uint32_t>(), ghist.as<uint32_t>(), nslots,
                      total.as<uint32_t>());
-  hipLaunchKernelGGL(k_bs_coarse, dim3(ntiles), dim3(256), 0, s, keys, vals, ne, fb_bits, ncb, ntiles,
-                     gbase.as<uint32_t>(), okeys.as<uint32_t>(), ovals.as<uint32_t>());
+  hipLaunchKernelGGL(k_bs_coarse, dim3(ntiles), dim3(256), (size_t)(2 * ncb + 2 * BS_TILE) * 4, s, keys, vals, ne,
+                     fb_bits, ncb, ntiles, gbase.as<uint32_t>(), okeys.as<uint32_t>(), ovals.as<uint32_t>());
   MSM_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(k_bs_fine, dim3(ncb), dim3(1024), 0, s, okeys.as<uint32_t>(), ovals.as<uint32_t>(), fb_bits, ncb,
                      ntiles, gbase.as<uint32_t>(), total.as<uint32_t>(), nb, sorted, counts, offsets);
   MSM_HIP_CHECK(hipGetLastError());
   classes.ensure(256 * 4);
   MSM_HIP_CHECK(hipMemsetAsync(classes.p, 0, 256 * 4, s));
-  hipLaunchKernelGGL(k_sched_hist, dim3(nblk(nb, 256)), dim3(256), 0, s, counts, nb, classes.as<uint32_t>());
+  hipLaunchKernelGGL(k_sched_hist, dim3(nblk(nb, SCHED_PER_BLOCK)), dim3(256), 0, s, counts, nb,
+                     classes.as<uint32_t>());
   hipLaunchKernelGGL(k_sched_scan, dim3(1), dim3(64), 0, s, classes.as<uint32_t>());
-  hipLaunchKernelGGL(k_sched_scatter, dim3(nblk(nb, 256)), dim3(256), 0, s, counts, nb, classes.as<uint32_t>(), order);
+  hipLaunchKernelGGL(k_sched_scatter, dim3(nblk(nb, SCHED_PER_BLOCK)), dim3(256), 0, s, counts, nb,
+                     classes.as<uint32_t>(), order);
   MSM_HIP_CHECK(hipGetLastError());
 }
 #endif
