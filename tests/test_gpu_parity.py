@@ -147,3 +147,55 @@ def test_msm_large_vs_reference(L, golden, group, n):
     assert m.compress(group, r).hex() == want
     # second call on the same context (buffers reused) gives the same answer
     assert ctx.mult(sc, 255) == r or m.compress(group, ctx.mult(sc, 255)).hex() == want
+
+
+R_ORDER = 0x73eda753299d7d483339d80809a1d80553bda402fffe5bfeffffffff00000001
+
+
+def _times_p0(m, k):
+    """k * P_0 (P_0 = fixed_points(1, 1)) by the CPU oracle, compressed."""
+    p0 = of.fixed_points(1, 1)
+    s = (ctypes.c_uint8 * 32).from_buffer_copy((k % R_ORDER).to_bytes(32, "little"))
+    return of.compress(1, of.msm(1, p0, s, 1, 255, "naive"))
+
+
+@pytest.mark.parametrize("n,kind", [(1 << 16, "pippenger"), (1 << 18, "pippenger"), (1 << 16, "ches")])
+def test_sort_heavy_bucket_equal_scalars(L, n, kind):
+    """Every scalar equal: each window's entries all land in ONE bucket, so one
+    coarse bin holds n entries -- the fine sort's LDS-window overflow path
+    (n = 2^16) and its unstaged fallback (n = 2^18, > BS_FINE_MAXW windows).
+    Expected value by linearity: s * sum P_i = s (2^n - 1) P_0 (P_i = 2^i P_0)."""
+    import msm_blst_amd as m
+    s0 = int.from_bytes(bytes(m.gen_scalars(1, 77)), "little")
+    sc = s0.to_bytes(32, "little") * n
+    pts = m.fixed_points(1, n)
+    if kind == "pippenger":
+        ctx = m.MSMContext(1, 0, 16)
+        ctx.set_points(pts, n)
+        r = ctx.mult(sc, 255)
+    else:
+        ctx = m.CHESContext(1, 0, n_exp=16)
+        ctx.build_table(pts, n)
+        r = ctx.mult(sc)
+    assert m.compress(1, r).hex() == _times_p0(m, s0 * ((1 << n) - 1))
+    ctx.close()
+
+
+def test_sort_heavy_bucket_mixed(L):
+    """Half the scalars equal (one heavy bucket per window beside ~13-entry
+    buckets): staged windows with entries past the LDS capacity."""
+    import msm_blst_amd as m
+    n = 1 << 17
+    rnd = bytes(m.gen_scalars(n, 5))
+    s0 = rnd[:32]
+    sc = bytearray(rnd)
+    for i in range(0, n, 2):
+        sc[32 * i:32 * i + 32] = s0
+    pts = m.fixed_points(1, n)
+    ctx = m.MSMContext(1, 0, 16)
+    ctx.set_points(pts, n)
+    got = m.compress(1, ctx.mult(bytes(sc), 255)).hex()
+    ctx.close()
+    P = of.fixed_points(1, n)
+    S = (ctypes.c_uint8 * len(sc)).from_buffer_copy(bytes(sc))
+    assert got == of.compress(1, of.msm(1, P, S, n, 255, "pippenger"))
