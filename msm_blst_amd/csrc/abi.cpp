@@ -895,14 +895,30 @@ size_t msm_ches_bucket_set(int q, int a_h, int *out, size_t cap) {
 
 int msm_ches_digit_table(int q, int a_h, digit_decomposition *out) {
   if (q < 4 || a_h < 0 || !out) return fail(MSM_E_ARG, "bad args");
-  std::vector<int> B = ches_bucket_set(q, a_h);
-  std::vector<uint32_t> H = ches_digit_hash(B, q);
-  for (size_t d = 0; d < H.size(); ++d) {
-    out[d].m = (int)((H[d] >> 24) & 3u) + 1;
-    out[d].b = B[H[d] & 0x00ffffffu];
-    out[d].alpha = (int)(H[d] >> 31);
+  try {
+    // decoded from the compact device tables (code + rank, ches_kernels.hpp)
+    // with the device's arithmetic, so the golden digit-table hashes pin them
+    std::vector<int> B = ches_bucket_set(q, a_h);
+    std::vector<uint32_t> code, rank;
+    ches_digit_code(B, q, code, rank);
+    for (size_t d = 0; d <= (size_t)q; ++d) {
+      const uint32_t c = (code[d >> 3] >> (4 * (d & 7))) & 15u, m = (c & 3u) + 1, alpha = (c >> 2) & 1u;
+      int b = 0;
+      if (!(c & 8u)) {
+        const uint32_t v = (alpha ? (uint32_t)q - (uint32_t)d : (uint32_t)d) / m;
+        const uint32_t bits = rank[2 * (v >> 5)], idx = rank[2 * (v >> 5) + 1] +
+                                                        (uint32_t)__builtin_popcount(bits & ((1u << (v & 31)) - 1u));
+        if (!((bits >> (v & 31)) & 1u)) return fail(MSM_E_ARG, "digit code names a value outside B");
+        b = B[idx];
+      }
+      out[d].m = (int)m;
+      out[d].b = b;
+      out[d].alpha = (int)alpha;
+    }
+    return MSM_OK;
+  } catch (const std::exception &e) {
+    return fail(MSM_E_ARG, e.what());
   }
-  return MSM_OK;
 }
 
 // ---------------- boundary helpers ----------------

@@ -198,7 +198,7 @@ static __global__ void __launch_bounds__(1024)
   for (int f = threadIdx.x; f < FB; f += blockDim.x) off[f] = 0;
   if (threadIdx.x <= BS_FINE_MAXW) wb[threadIdx.x] = nbin;
   __syncthreads();
-  constexpr int U = 8;  // loads in flight per thread
+  constexpr int U = 16, UW = 12;  // loads in flight per thread (histogram / window passes)
   for (uint32_t e0 = lo; e0 < hi; e0 += U * 1024) {
     uint32_t kk[U];
 #pragma unroll
@@ -253,20 +253,19 @@ static __global__ void __launch_bounds__(1024)
     uint32_t end = nbin;
     for (uint32_t j = k + 1; j < nwin; ++j)
       if (wb[j] < end) end = wb[j];
-    for (uint32_t e0 = lo; e0 < hi; e0 += U * 1024) {
-      uint32_t kk[U];
+    for (uint32_t e0 = lo; e0 < hi; e0 += UW * 1024) {
+      // keys and vals in one round trip (a dependent vals load per key would
+      // double the latency-bound passes); vals of other windows are re-read
+      uint32_t kk[UW], vv[UW];
 #pragma unroll
-      for (int r = 0; r < U; ++r) {
+      for (int r = 0; r < UW; ++r) {
         uint32_t e = e0 + threadIdx.x + r * 1024;
         kk[r] = e < hi ? okeys[e] : BS_NONE;
-        if (kk[r] != BS_NONE && win[kk[r] & fmask] != k) kk[r] = BS_NONE;
+        vv[r] = e < hi ? ovals[e] : 0u;
       }
-      uint32_t vv[U];
 #pragma unroll
-      for (int r = 0; r < U; ++r) vv[r] = kk[r] != BS_NONE ? ovals[e0 + threadIdx.x + r * 1024] : 0u;
-#pragma unroll
-      for (int r = 0; r < U; ++r) {
-        if (kk[r] == BS_NONE) continue;
+      for (int r = 0; r < UW; ++r) {
+        if (kk[r] == BS_NONE || win[kk[r] & fmask] != k) continue;
         uint32_t li = atomicAdd(&off[kk[r] & fmask], 1u) - base;
         if (li < (uint32_t)BS_FINE_CAP)
           stage[li] = vv[r];

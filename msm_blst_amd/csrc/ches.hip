@@ -100,6 +100,31 @@ std::vector<uint32_t> ches_digit_hash(const std::vector<int> &B, int q) {
       }
   return H;
 }
+
+void ches_digit_code(const std::vector<int> &B, int q, std::vector<uint32_t> &code, std::vector<uint32_t> &rank) {
+  const std::vector<uint32_t> H = ches_digit_hash(B, q);
+  code.assign(((size_t)q >> 3) + 2, 0);
+  for (size_t d = 0; d <= (size_t)q; ++d) {
+    const uint32_t m = ((H[d] >> 24) & 3u) + 1, alpha = H[d] >> 31;
+    const int b = B[H[d] & CH_IDX_MASK];
+    uint32_t c = (m - 1) | (alpha << 2);
+    if (b == 0) {
+      c |= 8u;  // bucket value 0: entry skipped
+    } else {
+      const long v = alpha ? (long)q - (long)d : (long)d;
+      if (v % m != 0 || v / m != b) throw std::runtime_error("CHES digit map is not arithmetic at d=" + std::to_string(d));
+    }
+    code[d >> 3] |= c << (4 * (d & 7));
+  }
+  const size_t words = ((size_t)B.back() >> 5) + 1;
+  rank.assign(2 * words, 0);
+  for (int v : B) rank[2 * ((size_t)v >> 5)] |= 1u << (v & 31);
+  uint32_t run = 0;
+  for (size_t w = 0; w < words; ++w) {
+    rank[2 * w + 1] = run;
+    run += (uint32_t)__builtin_popcount(rank[2 * w]);
+  }
+}
 #endif  // MSM_GROUP == 1
 
 // -------------------------------------------------------------- scan reduce --
@@ -298,9 +323,12 @@ Ches<G>::Ches(int device, const ChesParams &p) : dev_(device), p_(p) {
   if (p.b_size > 0 && (int)B_.size() != p.b_size)
     throw std::runtime_error("bucket set size " + std::to_string(B_.size()) + " != configured " +
                              std::to_string(p.b_size));
-  std::vector<uint32_t> H = ches_digit_hash(B_, q);
-  hash_.ensure(H.size() * 4);
-  MSM_HIP_CHECK(hipMemcpy(hash_.p, H.data(), H.size() * 4, hipMemcpyHostToDevice));
+  std::vector<uint32_t> code, rank;
+  ches_digit_code(B_, q, code, rank);
+  code_.ensure(code.size() * 4);
+  rank_.ensure(rank.size() * 4);
+  MSM_HIP_CHECK(hipMemcpy(code_.p, code.data(), code.size() * 4, hipMemcpyHostToDevice));
+  MSM_HIP_CHECK(hipMemcpy(rank_.p, rank.data(), rank.size() * 4, hipMemcpyHostToDevice));
   for (size_t k = 1; k < B_.size() && B_[k] <= p.a_h + 1; ++k) small_ = (int)k;
   plan_buckets(0);
   ev_.resize(8);
@@ -444,7 +472,7 @@ void Ches<G>::digits_sort(hipStream_t s, const uint8_t *d_scalars, size_t stride
   f.order.ensure(NB * 4);
 #define MSM_CHES_DIGITS(HT)                                                                                   \
   hipLaunchKernelGGL(k_ches_digits<HT>, dim3(nblk(n, 256)), dim3(256), 0, s, d_scalars, stride, n, p_.q_exp, p_.h, \
-                     hash_.as<uint32_t>(), f.keys.as<uint32_t>(), f.vals.as<uint32_t>(), (uint32_t)B_.size(),  \
+                     code_.as<uint32_t>(), rank_.as<uint2>(), f.keys.as<uint32_t>(), f.vals.as<uint32_t>(), (uint32_t)B_.size(),  \
                      (uint32_t)small_, (uint32_t)copies_)
   switch (p_.h) {  // the h of the reference configurations (ches_config_files)
     case 12: MSM_CHES_DIGITS(12); break;

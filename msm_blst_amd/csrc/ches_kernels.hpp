@@ -190,13 +190,22 @@ __device__ __forceinline__ void sub_r_if_ge(uint32_t s[8]) {
 // equal to sum s_i P_i for points of order r).
 // Top-digit entries whose bucket index k is <= small go to copy i % copies of
 // bucket k (copy 0 = k itself, copy c >= 1 = nb0 + (c-1) small + k - 1).
-// HT = compile-time digit count (fully unrolled: every hash lookup, H[d] and
-// H[d + 1] for both carry states, is issued before the carry chain resolves);
-// HT = 0 handles any h with a runtime loop.
+// HT = compile-time digit count (fully unrolled: every code lookup, for both
+// carry states, is issued before the carry chain resolves, then every rank
+// lookup); HT = 0 handles any h with a runtime loop.
+//
+// Digit code (replaces a gather from the (q+1)-entry, 16 MiB hash H of ref
+// main_p1.cpp:140-152, whose random 4-B reads missed L2 and cost 0.17 ms at
+// 2^20): H[d] = (m, b, alpha) always has b = (alpha ? q - d : d) / m
+// (ches_digit_code checks this on the host), so the device keeps only
+//   code[d]: 4 bits, (m - 1) | alpha << 2 | (b == 0) << 3, 8 per word (2 MiB)
+//   rank[v >> 5] = {bit v & 31 set iff v in B, #B below 32 (v >> 5)} (512 KiB)
+// and computes idx(b) = prefix + popcount(bits below b): both tables stay in
+// each XCD's 4 MiB L2.
 template <int HT>
 static __global__ void __launch_bounds__(256)
     k_ches_digits(const uint8_t *__restrict__ scalars, size_t stride, size_t n, int q_exp, int h_rt,
-                  const uint32_t *__restrict__ hash, uint32_t *__restrict__ keys, uint32_t *__restrict__ vals,
+                  const uint32_t *__restrict__ code, const uint2 *__restrict__ rank, uint32_t *__restrict__ keys, uint32_t *__restrict__ vals,
                   uint32_t nb0, uint32_t small, uint32_t copies) {
   const int h = HT ? HT : h_rt;
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -238,27 +247,49 @@ static __global__ void __launch_bounds__(256)
       keys[k] = KEY_NONE;
     }
   };
+  const uint32_t q = 1u << q_exp;
+  // code pair (d, d + 1) -> the carry-resolved (m - 1 | alpha << 2 | zero << 3, b)
+  auto pair = [&](uint32_t d) -> uint64_t {
+    const uint2 w = *reinterpret_cast<const uint2 *>(code + (d >> 3));  // 4-B aligned 8-B load
+    return ((((uint64_t)w.y << 32) | w.x) >> (4 * (d & 7))) & 0xffu;
+  };
+  auto resolve = [&](uint32_t d, uint32_t c, uint32_t &b) {
+    const uint32_t m1 = c & 3u, alpha = (c >> 2) & 1u;
+    uint32_t v = alpha ? q - d : d;
+    b = m1 == 0 ? v : (m1 == 1 ? v >> 1 : v / 3u);
+  };
+  auto entry = [&](uint32_t c, uint32_t b) -> uint32_t {
+    if (c & 8u) return 0u;
+    const uint2 r = rank[b >> 5];
+    const uint32_t idx = r.y + (uint32_t)__popc(r.x & ((1u << (b & 31)) - 1u));
+    return idx | ((c & 3u) << 24) | ((c & 4u) << 29);
+  };
   if constexpr (HT > 0) {
-    uint32_t e0[HT], e1[HT];
+    uint32_t dj[HT], cj[HT], bj[HT];
 #pragma unroll
     for (int j = 0; j < HT; ++j) {
-      uint32_t d = digit(j);
-      e0[j] = hash[d];
-      e1[j] = hash[d + 1];
+      dj[j] = digit(j);
+      cj[j] = (uint32_t)pair(dj[j]);  // low nibble: code[d], high: code[d + 1]
     }
     uint32_t carry = 0;
 #pragma unroll
     for (int j = 0; j < HT; ++j) {
-      uint32_t e = carry ? e1[j] : e0[j];
-      carry = e >> 31;
-      emit(j, e);
+      const uint32_t c = carry ? cj[j] >> 4 : cj[j] & 15u;
+      resolve(dj[j] + carry, c, bj[j]);
+      cj[j] = c;
+      carry = (c >> 2) & 1u;
     }
+#pragma unroll
+    for (int j = 0; j < HT; ++j) emit(j, entry(cj[j], bj[j]));
   } else {
     uint32_t carry = 0;
     for (int j = 0; j < h; ++j) {
-      uint32_t e = hash[digit(j) + carry];
-      carry = e >> 31;
-      emit(j, e);
+      const uint32_t d = digit(j) + carry;
+      const uint32_t c = (uint32_t)pair(d) & 15u;
+      uint32_t b;
+      resolve(d, c, b);
+      carry = (c >> 2) & 1u;
+      emit(j, entry(c, b));
     }
   }
 }

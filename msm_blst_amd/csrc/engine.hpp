@@ -109,6 +109,11 @@ bool ches_params_for(int n_exp, int beta, ChesParams *out);
 std::vector<int> ches_bucket_set(int q, int a_h);
 // packed digit hash (ches_kernels.hpp layout) of ref main_p1.cpp:140-152, q+1 entries
 std::vector<uint32_t> ches_digit_hash(const std::vector<int> &B, int q);
+// The same map in the compact device form (ches_kernels.hpp "digit code"):
+// a 4-bit code per digit value, 8 per word, (q >> 3) + 2 words, and the rank
+// table {membership bits, prefix count} per 32 values of [0, max B].  Throws if
+// some H[d] is not (m, (alpha ? q - d : d) / m, alpha).
+void ches_digit_code(const std::vector<int> &B, int q, std::vector<uint32_t> &code, std::vector<uint32_t> &rank);
 
 // Low-depth dense reduction: for each of W windows of S buckets (A[w*S + b-1]
 // holds bucket value b, S a power of two), T_w = sum_b b A_b computed as the sum
@@ -242,7 +247,7 @@ class Ches {
   void plan_buckets(size_t n);
   bool profile_ = false;
   PhaseTimes times_;
-  DevBuf hash_, table_, buckets_[2];  // buckets double-buffered: MSM k's reduction reads set k&1
+  DevBuf code_, rank_, table_, buckets_[2];  // buckets double-buffered: MSM k's reduction reads set k&1
   // digit/sort outputs, double-buffered so that MSM k+1's digits and sort
   // (memory/LDS-bound) run beside MSM k's accumulation (VALU-bound) in a batch
   ChesFrontSet fs_[2];

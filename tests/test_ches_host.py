@@ -62,3 +62,18 @@ def test_driver_tables_n10(ches, golden):
     assert list(ches.bucket_set(q, 231)) == g["bucket_set"]
     H = ches.digit_table(q, 231)
     assert [[H[v].m, H[v].b, H[v].alpha] for v in range(q + 1)] == g["digit_table"]
+
+
+@pytest.mark.parametrize("cfg", [20, 16])
+def test_device_digit_code_matches_oracle_table(ches, golden, cfg):
+    """The device's compact digit code + rank tables, decoded with the device
+    arithmetic (msm_ches_digit_table), equal the oracle's digit hash entry for
+    entry (ref main_p1.cpp:140-152) over the whole digit range."""
+    import numpy as np
+    import oracle_ffi as of
+    g = golden(f"ches_params_n{cfg}.json")
+    q = 1 << g["q_exp"]
+    got = np.frombuffer(bytes(ches.digit_table(q, g["a_h"])), dtype=np.int32)
+    H, _ = of.digit_table(of.bucket_set(q, g["a_h"]), q)
+    want = np.frombuffer(bytes(H), dtype=np.int32)
+    assert got.shape == want.shape and np.array_equal(got, want)
