@@ -579,9 +579,13 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *d_scalars, size_t stride, 
       MSM_HIP_CHECK(hipEventCreate(&e));
       acc_ev_.push_back(e);
     }
-  // Four streams, two buffer sets (set = k & 1):
-  //   fstream_:  digits + sort of MSM k into front set k&1 (after MSM k-2's
-  //              accumulation released it) -- overlaps MSM k-1's accumulation;
+  // Four streams, three front sets (k % 3) and two bucket sets (k & 1):
+  //   fstream_:  digits + sort of MSM k into front set k%3 (after MSM k-3's
+  //              accumulation released it).  The accumulation fills every CU
+  //              slot until its last workgroups are dispatched, so a front only
+  //              gets the chip in an accumulation's tail: with three sets, MSM
+  //              k+1's front runs in MSM k-1's tail, not in MSM k's, and is
+  //              ready before MSM k's accumulation ends;
   //   s:         accumulation k into bucket set k&1 (after MSM k-2's reduction
   //              head released it) -- back to back, the VALU-bound critical path;
   //   tails_[set]: the whole reduction of MSM k (level 0, latency-bound tail,
@@ -597,14 +601,14 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *d_scalars, size_t stride, 
   MSM_HIP_CHECK(hipEventRecord(bev_[0], s));  // the batch starts after prior work on s
   MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, bev_[0], 0));
   for (size_t k = 0; k < count; ++k) {
-    const int set = (int)(k & 1);
-    if (k >= 2) MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, eva[k - 2], 0));  // front set free again
-    digits_sort(fstream_, d_scalars + k * set_stride, stride, set);
+    const int set = (int)(k & 1), fset = (int)(k % kFronts);
+    if (k >= (size_t)kFronts) MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, eva[k - kFronts], 0));  // front set free
+    digits_sort(fstream_, d_scalars + k * set_stride, stride, fset);
     MSM_HIP_CHECK(hipEventRecord(evf[k], fstream_));
     MSM_HIP_CHECK(hipStreamWaitEvent(s, evf[k], 0));
     if (k >= 2) MSM_HIP_CHECK(hipStreamWaitEvent(s, evh[k - 2], 0));  // bucket set free again
     if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k], s));
-    accumulate(s, set, set);
+    accumulate(s, fset, set);
     if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k + 1], s));
     MSM_HIP_CHECK(hipEventRecord(eva[k], s));
     MSM_HIP_CHECK(hipStreamWaitEvent(tails_[set], eva[k], 0));

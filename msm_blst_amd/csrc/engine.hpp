@@ -250,7 +250,8 @@ class Ches {
   DevBuf code_, rank_, table_, buckets_[2];  // buckets double-buffered: MSM k's reduction reads set k&1
   // digit/sort outputs, double-buffered so that MSM k+1's digits and sort
   // (memory/LDS-bound) run beside MSM k's accumulation (VALU-bound) in a batch
-  ChesFrontSet fs_[2];
+  static constexpr int kFronts = 3;  // batch: front k+1 runs in MSM k-1's accumulation tail
+  ChesFrontSet fs_[kFronts];
   WeightedReducer<G> red_;
   std::vector<hipEvent_t> ev_;
   hipStream_t tails_[2] = {nullptr, nullptr}, fstream_ = nullptr;
