@@ -4,13 +4,13 @@
 FETCH_SIZE/WRITE_SIZE are in KiB.  MI355X_MICROARCH.md (HBM section): on gfx950
 FETCH_SIZE reports half the bytes of wide (16 B/lane) reads -> x2; WRITE_SIZE
 is exact for 16 B/lane stores.  Our gathers are 16 B/lane loads of 112-B rows.
-usage: python tools/pmc_traffic.py <counter_collection.csv> <method> <log_n> [out.json]
+usage: python tools/pmc_traffic.py <counter_collection.csv[,second_pass.csv]> <method> <log_n> [out.json]
 """
 import csv
 import json
 import sys
 
-rows = list(csv.DictReader(open(sys.argv[1])))
+rows = [r for f in sys.argv[1].split(",") for r in csv.DictReader(open(f))]
 vals = {}
 for r in rows:
     if "k_accumulate" not in r["Kernel_Name"]:
