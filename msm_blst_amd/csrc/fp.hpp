@@ -293,22 +293,24 @@ struct Fp2 {
   Fp c0, c1;
 };
 
-// Karatsuba (ref no_asm.h:566-579): 3 Montgomery products, outputs reduced to S.
+// (a0 + a1 i)(b0 + b1 i) as two sums of products with one Montgomery reduction
+// each (fp_mul2), instead of Karatsuba's three products (ref no_asm.h:566-579):
+//   c0 = a0 b0 + a1 (8p - b1),   c1 = a0 b1 + a1 b0.
+// Same 1176 mads, but no add/sub/reduce fix-ups and two live temporaries
+// instead of five -- the G2 bucket accumulation is register-bound.
+// Ranges: a lazy (< 6p, limbs < 2^30); b lazy, normalized here (limbs < 2^28
+// below the top limb) so every column stays < 2^63.5 (14 a_i b_j < 2^61.8,
+// 14 a_i (8p - b1)_j < 2^62.8, 14 m p < 2^59.8); a b + a1 (8p - b1) < 84 p^2 ->
+// output normalized, < 1.1 p (class S).  r may alias a or b.
 __device__ __forceinline__ void f_mul(Fp2 &r, const Fp2 &a, const Fp2 &b) {
-  Fp t0, t1, sa, sb, t2;
-  fp_mul(t0, a.c0, b.c0);
-  fp_mul(t1, a.c1, b.c1);
-  fp_add(sa, a.c0, a.c1);
-  fp_add(sb, b.c0, b.c1);
-  fp_norm(sa);                     // component limbs may be < 2^29.6 (sub4 outputs): keep
-  fp_norm(sb);                     // mul-input limbs < 2^30 (column bound, see fp_mul)
-  fp_mul(t2, sa, sb);
-  fp_sub<4>(r.c0, t0, t1);
-  fp_nred(r.c0);
-  fp_sub<4>(t2, t2, t0);
-  fp_norm(t2);
-  fp_sub<4>(r.c1, t2, t1);
-  fp_nred(r.c1);
+  Fp b0 = b.c0, b1 = b.c1, nb1, t0, t1;
+  fp_norm(b0);
+  fp_norm(b1);
+  fp_neg<8>(nb1, b1);
+  fp_mul2(t0, a.c0, b0, a.c1, nb1);
+  fp_mul2(t1, a.c0, b1, a.c1, b0);
+  r.c0 = t0;
+  r.c1 = t1;
 }
 // (a0 + a1 i)^2 = (a0+a1)(a0-a1) + 2 a0 a1 i   (ref no_asm.h:638-688)
 __device__ __forceinline__ void f_sqr(Fp2 &r, const Fp2 &a) {
