@@ -140,13 +140,19 @@ __device__ __forceinline__ void xyzz_add(Xyzz<F> &acc, const Xyzz<F> &b) {
     acc = b;
     return;
   }
-  F U1, S1, P, R, PP, PPP, Q, t;
-  f_mul(U1, acc.x, b.zz);    // S
-  f_mul(S1, acc.y, b.zzz);   // S
-  f_mul(P, b.x, acc.zz);     // U2 S
-  f_mul(R, b.y, acc.zzz);    // S2 S
-  f_sub4(P, P, U1);          // < 6p
-  f_sub4(R, R, S1);          // < 6p
+  // Computed in place so that b dies early and at most ~8 field elements are
+  // live (G2: 28 VGPRs each): acc is first rewritten as the representative
+  // (U1, S1, ZZZ1 ZZZ2, ZZ1 ZZ2) of the same point, which is also what the
+  // doubling branch doubles.
+  F P, R, PP, PPP, t;
+  f_mul(acc.x, acc.x, b.zz);    // U1 = X1 ZZ2          S
+  f_mul(acc.y, acc.y, b.zzz);   // S1 = Y1 ZZZ2         S
+  f_mul(P, b.x, acc.zz);        // U2 = X2 ZZ1          S
+  f_sub4(P, P, acc.x);          // P = U2 - U1          < 6p
+  f_mul(R, b.y, acc.zzz);       // S2 = Y2 ZZZ1         S
+  f_sub4(R, R, acc.y);          // R = S2 - S1          < 6p
+  f_mul(acc.zz, acc.zz, b.zz);
+  f_mul(acc.zzz, acc.zzz, b.zzz);
   f_sqr(PP, P);
   if (__builtin_expect(f_is_zero_S(PP), 0)) {
     F RR;
@@ -159,24 +165,21 @@ __device__ __forceinline__ void xyzz_add(Xyzz<F> &acc, const Xyzz<F> &b) {
     }
     return;
   }
-  f_mul(PPP, PP, P);
-  f_mul(Q, U1, PP);
-  F X3, Y3;
+  f_mul(acc.zz, acc.zz, PP);    // ZZ3 = ZZ1 ZZ2 PP
+  f_mul(PPP, P, PP);
+  f_mul(acc.x, acc.x, PP);      // Q = U1 PP  (in place of U1)
+  f_mul(acc.zzz, acc.zzz, PPP); // ZZZ3 = ZZZ1 ZZZ2 PPP
+  F X3;
   f_sqr(X3, R);
   f_sub4(X3, X3, PPP);
   f_norm(X3);
-  f_sub4(X3, X3, Q);
+  f_sub4(X3, X3, acc.x);
   f_norm(X3);
-  f_sub4(X3, X3, Q);
-  f_nred(X3);
-  f_sub4(t, Q, X3);
-  f_mul_sub(Y3, t, R, S1, PPP);  // R (Q - X3) - S1 PPP   S (one reduction)
-  f_mul(acc.zz, acc.zz, b.zz);
-  f_mul(acc.zz, acc.zz, PP);
-  f_mul(acc.zzz, acc.zzz, b.zzz);
-  f_mul(acc.zzz, acc.zzz, PPP);
+  f_sub4(X3, X3, acc.x);
+  f_nred(X3);                   // X3 = R^2 - PPP - 2Q  S
+  f_sub4(t, acc.x, X3);
+  f_mul_sub(acc.y, t, R, acc.y, PPP);  // Y3 = R (Q - X3) - S1 PPP   S (one reduction)
   acc.x = X3;
-  acc.y = Y3;
 }
 
 }  // namespace msm

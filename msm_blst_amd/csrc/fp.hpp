@@ -128,6 +128,45 @@ __device__ __forceinline__ void fp_mul2(Fp &r, const Fp &a, const Fp &b, const F
   r.v[NL - 1] = (uint32_t)acc;
 }
 
+// Four products with ONE Montgomery reduction: (a b + c d + e f + g h) / R mod p.
+// The caller keeps every column < 2^64: 14 (a_i b_j + c_i d_j + e_i f_j + g_i h_j)
+// + 14 m p + carry (see the Fp2 f_mul_sub below for the ranges it uses).
+__device__ __forceinline__ void fp_mul4(Fp &r, const Fp &a, const Fp &b, const Fp &c, const Fp &d, const Fp &e,
+                                        const Fp &f, const Fp &g, const Fp &h) {
+  uint32_t m[NL];
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {
+#pragma unroll
+    for (int i = 0; i <= k; ++i) {
+      acc = mad64(a.v[i], b.v[k - i], acc);
+      acc = mad64(c.v[i], d.v[k - i], acc);
+      acc = mad64(e.v[i], f.v[k - i], acc);
+      acc = mad64(g.v[i], h.v[k - i], acc);
+    }
+#pragma unroll
+    for (int i = 0; i < k; ++i) acc = mad64(m[i], P28[k - i], acc);
+    m[k] = ((uint32_t)acc * N0P) & MASK;
+    acc = mad64(m[k], P28[0], acc);
+    acc >>= 28;
+  }
+#pragma unroll
+  for (int k = NL; k < 2 * NL - 1; ++k) {
+#pragma unroll
+    for (int i = k - NL + 1; i < NL; ++i) {
+      acc = mad64(a.v[i], b.v[k - i], acc);
+      acc = mad64(c.v[i], d.v[k - i], acc);
+      acc = mad64(e.v[i], f.v[k - i], acc);
+      acc = mad64(g.v[i], h.v[k - i], acc);
+    }
+#pragma unroll
+    for (int i = k - NL + 1; i < NL; ++i) acc = mad64(m[i], P28[k - i], acc);
+    r.v[k - NL] = (uint32_t)acc & MASK;
+    acc >>= 28;
+  }
+  r.v[NL - 1] = (uint32_t)acc;
+}
+
 // Montgomery square: cross products once, doubled (limbs < 2^29 so 2a_i < 2^30).
 __device__ __forceinline__ void fp_sqr(Fp &r, const Fp &a) {
   uint32_t m[NL], a2[NL];
@@ -340,13 +379,24 @@ __device__ __forceinline__ void f_zero(Fp2 &r) { fp_zero(r.c0); fp_zero(r.c1); }
 __device__ __forceinline__ bool f_is_zero_exact(const Fp2 &a) { return fp_is_zero_exact(a.c0) && fp_is_zero_exact(a.c1); }
 __device__ __forceinline__ bool f_is_zero_S(const Fp2 &a) { return fp_is_zero_lt2p(a.c0) && fp_is_zero_lt2p(a.c1); }
 __device__ __forceinline__ void f_mul3(Fp2 &r, const Fp2 &a) { f_mul3(r.c0, a.c0); f_mul3(r.c1, a.c1); }
-// a b - c d over Fp2 (two Karatsuba products, then one subtraction) -> S
+// a b - c d over Fp2, each component one four-product reduction (fp_mul4):
+//   r0 = a0 b0 + a1 (8p - b1) + c0 (8p - d0) + c1 d1
+//   r1 = a0 b1 + a1 b0 + c0 (8p - d1) + c1 (8p - d0)
+// Ranges (every caller: xyzz Y3 lines): a lazy (< 6p, limbs < 2^29.6), b lazy
+// (normalized here), c, d in S.  Column < 14 (2^57.6 + 2^58.6 + 2^57 + 2^57)
+// + 14 m p < 2^63.6; value < 104 p^2 -> output normalized, < 1.1 p (S).
+// r may alias any input.
 __device__ __forceinline__ void f_mul_sub(Fp2 &r, const Fp2 &a, const Fp2 &b, const Fp2 &c, const Fp2 &d) {
-  Fp2 t, u;
-  f_mul(t, a, b);
-  f_mul(u, c, d);
-  f_sub4(r, t, u);
-  f_nred(r);
+  Fp b0 = b.c0, b1 = b.c1, nb1, nd0, nd1, t0, t1;
+  fp_norm(b0);
+  fp_norm(b1);
+  fp_neg<8>(nb1, b1);
+  fp_neg<8>(nd0, d.c0);
+  fp_neg<8>(nd1, d.c1);
+  fp_mul4(t0, a.c0, b0, a.c1, nb1, c.c0, nd0, c.c1, d.c1);
+  fp_mul4(t1, a.c0, b1, a.c1, b0, c.c0, nd1, c.c1, nd0);
+  r.c0 = t0;
+  r.c1 = t1;
 }
 
 }  // namespace msm
