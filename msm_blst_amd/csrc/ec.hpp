@@ -95,8 +95,8 @@ __device__ __forceinline__ void xyzz_madd(Xyzz<F> &acc, const Aff<F> &p, bool ne
   } else {
     y2 = p.y;
   }
-  f_mul(P, p.x, acc.zz);   // U2 = X2 ZZ1          S
-  f_mul(R, y2, acc.zzz);   // S2 = Y2 ZZZ1         S
+  f_mul_bs(P, p.x, acc.zz);   // U2 = X2 ZZ1          S
+  f_mul_bs(R, y2, acc.zzz);   // S2 = Y2 ZZZ1         S
   f_sub4(P, P, acc.x);     // P = U2 - X1          < 6p lazy
   f_sub4(R, R, acc.y);     // R = S2 - Y1          < 6p lazy
   f_sqr(PP, P);            // PP                   S
@@ -114,11 +114,12 @@ __device__ __forceinline__ void xyzz_madd(Xyzz<F> &acc, const Aff<F> &p, bool ne
     return;
   }
   // ordered so that ZZ1, P, X1 and PP die as early as possible (register
-  // pressure: 8-10 live field elements; G2 elements are 28 VGPRs each)
-  f_mul(acc.zz, acc.zz, PP);    // ZZ3 = ZZ1 PP         S
-  f_mul(PPP, PP, P);            // S
-  f_mul(acc.x, acc.x, PP);      // Q = X1 PP  (in place of X1)   S
-  f_mul(acc.zzz, acc.zzz, PPP); // ZZZ3 = ZZZ1 PPP      S
+  // pressure: 8-10 live field elements; G2 elements are 28 VGPRs each);
+  // f_mul_bs: second operand normalized (every S value here)
+  f_mul_bs(acc.zz, acc.zz, PP);    // ZZ3 = ZZ1 PP         S
+  f_mul_bs(PPP, P, PP);         // S
+  f_mul_bs(acc.x, acc.x, PP);      // Q = X1 PP  (in place of X1)   S
+  f_mul_bs(acc.zzz, acc.zzz, PPP); // ZZZ3 = ZZZ1 PPP      S
   F X3;
   f_sqr(X3, R);            // R^2                  S
   f_sub4(X3, X3, PPP);     // < 6p
@@ -145,14 +146,14 @@ __device__ __forceinline__ void xyzz_add(Xyzz<F> &acc, const Xyzz<F> &b) {
   // (U1, S1, ZZZ1 ZZZ2, ZZ1 ZZ2) of the same point, which is also what the
   // doubling branch doubles.
   F P, R, PP, PPP, t;
-  f_mul(acc.x, acc.x, b.zz);    // U1 = X1 ZZ2          S
-  f_mul(acc.y, acc.y, b.zzz);   // S1 = Y1 ZZZ2         S
-  f_mul(P, b.x, acc.zz);        // U2 = X2 ZZ1          S
+  f_mul_bs(acc.x, acc.x, b.zz);    // U1 = X1 ZZ2          S
+  f_mul_bs(acc.y, acc.y, b.zzz);   // S1 = Y1 ZZZ2         S
+  f_mul_bs(P, b.x, acc.zz);        // U2 = X2 ZZ1          S
   f_sub4(P, P, acc.x);          // P = U2 - U1          < 6p
-  f_mul(R, b.y, acc.zzz);       // S2 = Y2 ZZZ1         S
+  f_mul_bs(R, b.y, acc.zzz);       // S2 = Y2 ZZZ1         S
   f_sub4(R, R, acc.y);          // R = S2 - S1          < 6p
-  f_mul(acc.zz, acc.zz, b.zz);
-  f_mul(acc.zzz, acc.zzz, b.zzz);
+  f_mul_bs(acc.zz, acc.zz, b.zz);
+  f_mul_bs(acc.zzz, acc.zzz, b.zzz);
   f_sqr(PP, P);
   if (__builtin_expect(f_is_zero_S(PP), 0)) {
     F RR;
@@ -165,10 +166,10 @@ __device__ __forceinline__ void xyzz_add(Xyzz<F> &acc, const Xyzz<F> &b) {
     }
     return;
   }
-  f_mul(acc.zz, acc.zz, PP);    // ZZ3 = ZZ1 ZZ2 PP
-  f_mul(PPP, P, PP);
-  f_mul(acc.x, acc.x, PP);      // Q = U1 PP  (in place of U1)
-  f_mul(acc.zzz, acc.zzz, PPP); // ZZZ3 = ZZZ1 ZZZ2 PPP
+  f_mul_bs(acc.zz, acc.zz, PP);    // ZZ3 = ZZ1 ZZ2 PP
+  f_mul_bs(PPP, P, PP);
+  f_mul_bs(acc.x, acc.x, PP);      // Q = U1 PP  (in place of U1)
+  f_mul_bs(acc.zzz, acc.zzz, PPP); // ZZZ3 = ZZZ1 ZZZ2 PPP
   F X3;
   f_sqr(X3, R);
   f_sub4(X3, X3, PPP);

@@ -351,6 +351,18 @@ __device__ __forceinline__ void f_mul(Fp2 &r, const Fp2 &a, const Fp2 &b) {
   r.c0 = t0;
   r.c1 = t1;
 }
+// f_mul for a b already normalized (class S, or any normalized value < 8p):
+// no normalized copies of b, one temporary (fp_mul2 writes limb j only after
+// its last read of limb j of any input, so r.c1 may be produced in place).
+__device__ __forceinline__ void f_mul_bs(Fp2 &r, const Fp2 &a, const Fp2 &b) {
+  Fp nb1, t0;
+  fp_neg<8>(nb1, b.c1);
+  fp_mul2(t0, a.c0, b.c0, a.c1, nb1);
+  fp_mul2(r.c1, a.c0, b.c1, a.c1, b.c0);
+  r.c0 = t0;
+}
+__device__ __forceinline__ void f_mul_bs(Fp &r, const Fp &a, const Fp &b) { fp_mul(r, a, b); }
+
 // (a0 + a1 i)^2 = (a0+a1)(a0-a1) + 2 a0 a1 i   (ref no_asm.h:638-688)
 __device__ __forceinline__ void f_sqr(Fp2 &r, const Fp2 &a) {
   Fp s, d, m, a1 = a.c1;
