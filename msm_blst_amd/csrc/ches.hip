@@ -17,6 +17,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "ches_kernels.hpp"
@@ -351,6 +352,7 @@ Ches<G>::~Ches() {
   for (int k = 0; k < 2; ++k)
     if (tails_[k]) (void)hipStreamDestroy(tails_[k]);
   if (fstream_) (void)hipStreamDestroy(fstream_);
+  if (accs_) (void)hipStreamDestroy(accs_);
 }
 
 // bucket space = B plus (copies_ - 1) copies of the small buckets 1..small_;
@@ -553,8 +555,12 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *d_scalars, size_t stride, 
     // long accumulation's pending workgroups: highest stream priority
     int least = 0, greatest = 0;
     MSM_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    for (int k = 0; k < 2; ++k) MSM_HIP_CHECK(hipStreamCreateWithPriority(&tails_[k], hipStreamNonBlocking, greatest));
+    const char *bm = std::getenv("MSM_BATCH_MODE");
+    bmode_ = bm ? std::atoi(bm) : 0;
+    for (int k = 0; k < 2; ++k)
+      MSM_HIP_CHECK(hipStreamCreateWithPriority(&tails_[k], hipStreamNonBlocking, (bmode_ & 2) ? least : greatest));
     MSM_HIP_CHECK(hipStreamCreateWithPriority(&fstream_, hipStreamNonBlocking, greatest));
+    if (bmode_ & 4) MSM_HIP_CHECK(hipStreamCreateWithPriority(&accs_, hipStreamNonBlocking, greatest));
     for (int k = 0; k < 2; ++k) {
       MSM_HIP_CHECK(hipEventCreateWithFlags(&ev_head_[k], hipEventDisableTiming));
       MSM_HIP_CHECK(hipEventCreateWithFlags(&ev_tail_[k], hipEventDisableTiming));
@@ -600,18 +606,32 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *d_scalars, size_t stride, 
   hipEvent_t *evf = bev_.data() + 1, *eva = evf + count, *evh = eva + count;  // front, acc, head of MSM k
   MSM_HIP_CHECK(hipEventRecord(bev_[0], s));  // the batch starts after prior work on s
   MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, bev_[0], 0));
-  for (size_t k = 0; k < count; ++k) {
-    const int set = (int)(k & 1), fset = (int)(k % kFronts);
+  auto issue_front = [&](size_t k) {
     if (k >= (size_t)kFronts) MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, eva[k - kFronts], 0));  // front set free
-    digits_sort(fstream_, d_scalars + k * set_stride, stride, fset);
+    digits_sort(fstream_, d_scalars + k * set_stride, stride, (int)(k % kFronts));
     MSM_HIP_CHECK(hipEventRecord(evf[k], fstream_));
-    MSM_HIP_CHECK(hipStreamWaitEvent(s, evf[k], 0));
-    if (k >= 2) MSM_HIP_CHECK(hipStreamWaitEvent(s, evh[k - 2], 0));  // bucket set free again
-    if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k], s));
-    accumulate(s, fset, set);
-    if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k + 1], s));
-    MSM_HIP_CHECK(hipEventRecord(eva[k], s));
+  };
+  hipStream_t as = accs_ ? accs_ : s;
+  if (accs_) MSM_HIP_CHECK(hipStreamWaitEvent(accs_, bev_[0], 0));
+  const bool front_first = bmode_ & 1;
+  if (front_first) issue_front(0);
+  for (size_t k = 0; k < count; ++k) {
+    if (!front_first) issue_front(k);
+    const int set = (int)(k & 1), fset = (int)(k % kFronts);
+    MSM_HIP_CHECK(hipStreamWaitEvent(as, evf[k], 0));
+    if (k >= 2) MSM_HIP_CHECK(hipStreamWaitEvent(as, evh[k - 2], 0));  // bucket set free again
+    if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k], as));
+    accumulate(as, fset, set);
+    if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k + 1], as));
+    MSM_HIP_CHECK(hipEventRecord(eva[k], as));
+    // front k+1 is issued before head k and head k waits for it: at the end of
+    // accumulation k both are ready, and a head dispatched first holds the
+    // dispatcher for its whole grid (~0.4 ms) while accumulation k+1 waits on
+    // its front (measured: profiles/r01f timeline).  Front first, then head k
+    // beside accumulation k+1.
+    if (front_first && k + 1 < count) issue_front(k + 1);
     MSM_HIP_CHECK(hipStreamWaitEvent(tails_[set], eva[k], 0));
+    if (front_first && k + 1 < count) MSM_HIP_CHECK(hipStreamWaitEvent(tails_[set], evf[k + 1], 0));
     red_.launch_head(tails_[set], buckets_[set].p, set);
     MSM_HIP_CHECK(hipEventRecord(evh[k], tails_[set]));
     red_.launch_tail(tails_[set], set, false);  // beside the accumulations: least resource time
