@@ -56,7 +56,12 @@ Pippenger<G> &tls_engine(int window) {
   return *it->second;
 }
 
-// gather the {ptr,NULL}-or-pointer-array inputs into flat host arrays
+// gather the pointer-array inputs into flat host arrays with the reference's
+// iteration rule (ref multi_scalar.c:390-416): the first pointer is always
+// taken; after it, a non-NULL entry names the next element and a NULL entry
+// means "the element right after the previous one" -- so {ptr, NULL} is one
+// flat array and a NULL after k explicit pointers continues contiguously.
+// Scalars advance by nbytes = (nbits+7)/8 (multi_scalar.c:395).
 template <int G>
 void gather(std::vector<uint8_t> &pts, std::vector<uint8_t> &sc, const void *const *points, size_t n,
             const byte *const *scalars, size_t nbits) {
@@ -64,15 +69,17 @@ void gather(std::vector<uint8_t> &pts, std::vector<uint8_t> &sc, const void *con
   pts.resize(n * psz);
   sc.resize(n * nb);
   if (n == 0) return;
-  if (n == 1 || points[1] == nullptr) {
-    memcpy(pts.data(), points[0], n * psz);
-  } else {
-    for (size_t i = 0; i < n; ++i) memcpy(pts.data() + i * psz, points[i], psz);
-  }
-  if (n == 1 || scalars[1] == nullptr) {
-    memcpy(sc.data(), scalars[0], n * nb);
-  } else {
-    for (size_t i = 0; i < n; ++i) memcpy(sc.data() + i * nb, scalars[i], nb);
+  const uint8_t *p = (const uint8_t *)*points++;
+  const uint8_t *s = *scalars++;
+  memcpy(pts.data(), p, psz);
+  memcpy(sc.data(), s, nb);
+  for (size_t i = 1; i < n; ++i) {
+    // the reference reads points[i] / scalars[i] only while the previous ones
+    // were non-NULL (multi_scalar.c:413: `*points ? *points++ : point+1`)
+    p = *points ? (const uint8_t *)*points++ : p + psz;
+    s = *scalars ? *scalars++ : s + nb;
+    memcpy(pts.data() + i * psz, p, psz);
+    memcpy(sc.data() + i * nb, s, nb);
   }
 }
 
@@ -267,6 +274,7 @@ void fixed_points(hfp::Aff<F> *out, size_t n, hfp::Jac<F> g) {
 struct msm_ches_ctx {
   int group = 1;
   int device = 0;
+  bool ready = false;  // a table was built / set / loaded (mult before that: MSM_E_STATE)
   std::unique_ptr<Ches<1>> g1;
   std::unique_ptr<Ches<2>> g2;
   DevBuf scalars;
@@ -275,6 +283,7 @@ struct msm_ches_ctx {
 struct msm_bgmw_ctx {
   int group = 1;
   int device = 0;
+  bool ready = false;
   std::unique_ptr<Bgmw<1>> g1;
   std::unique_ptr<Bgmw<2>> g2;
   DevBuf scalars;
@@ -334,20 +343,40 @@ static int load_table_file(E &eng, int group, int method, int q_exp, int h, cons
     fclose(f);
     return fail(MSM_E_ARG, "table file was written for other parameters");
   }
-  eng.reserve_table((size_t)hd.npoints);
-  if (eng.table_rows() != hd.rows) {
+  // validate everything the header claims before the engine is touched: the
+  // row count must be the method's (3 h per point for CHES, h for BGMW95) and
+  // the file must hold exactly header + rows * affine bytes
+  const uint64_t per_point = (uint64_t)(method == 1 ? 3 : 1) * (uint64_t)h;
+  const uint64_t row_bytes = 96ull * (uint64_t)group;
+  if (hd.npoints >= (1ull << 31) || hd.rows != per_point * hd.npoints) {
     fclose(f);
     return fail(MSM_E_ARG, "table file row count does not match its point count");
   }
-  std::vector<uint8_t> buf(std::min<size_t>(kTableChunk, std::max<size_t>(hd.rows, 1)) * 96 * group);
+  if (fseek(f, 0, SEEK_END) != 0 || (uint64_t)ftell(f) != sizeof hd + hd.rows * row_bytes ||
+      fseek(f, (long)sizeof hd, SEEK_SET) != 0) {
+    fclose(f);
+    return fail(MSM_E_ARG, std::string("table file size does not match its header: ") + path);
+  }
   bool ok = true;
-  for (size_t r0 = 0; ok && r0 < hd.rows; r0 += kTableChunk) {
-    size_t cnt = std::min(kTableChunk, (size_t)hd.rows - r0);
-    ok = fread(buf.data(), 96 * group, cnt, f) == cnt;
-    if (ok) eng.put_table(buf.data(), r0, cnt, false, (hipStream_t)0);
+  try {
+    eng.reserve_table((size_t)hd.npoints);
+    std::vector<uint8_t> buf(std::min<size_t>(kTableChunk, std::max<size_t>(hd.rows, 1)) * row_bytes);
+    for (size_t r0 = 0; ok && r0 < hd.rows; r0 += kTableChunk) {
+      size_t cnt = std::min(kTableChunk, (size_t)hd.rows - r0);
+      ok = fread(buf.data(), row_bytes, cnt, f) == cnt;
+      if (ok) eng.put_table(buf.data(), r0, cnt, false, (hipStream_t)0);
+    }
+  } catch (...) {
+    fclose(f);
+    eng.reserve_table(0);  // no half-loaded table: the context has no points until a good load/build
+    throw;
   }
   fclose(f);
-  return ok ? MSM_OK : fail(MSM_E_ARG, std::string("short read: ") + path);
+  if (!ok) {
+    eng.reserve_table(0);
+    return fail(MSM_E_ARG, std::string("short read: ") + path);
+  }
+  return MSM_OK;
 }
 
 }  // namespace
@@ -642,7 +671,9 @@ int msm_ches_ctx_create(msm_ches_ctx **ctx, int group, int device, int n_exp, in
 int msm_ches_ctx_build_table(msm_ches_ctx *ctx, const void *pts, size_t n, int on_device, void *stream) {
   if (!ctx || (!pts && n)) return fail(MSM_E_ARG, "bad args");
   try {
+    ctx->ready = false;
     CHES_DISPATCH(ctx, build_table(pts, n, on_device != 0, (hipStream_t)stream));
+    ctx->ready = true;
     return MSM_OK;
   } catch (const std::exception &e) {
     return fail(MSM_E_HIP, e.what());
@@ -652,7 +683,9 @@ int msm_ches_ctx_build_table(msm_ches_ctx *ctx, const void *pts, size_t n, int o
 int msm_ches_ctx_set_table(msm_ches_ctx *ctx, const void *tab, size_t n, int on_device, void *stream) {
   if (!ctx || (!tab && n)) return fail(MSM_E_ARG, "bad args");
   try {
+    ctx->ready = false;
     CHES_DISPATCH(ctx, set_table(tab, n, on_device != 0, (hipStream_t)stream));
+    ctx->ready = true;
     return MSM_OK;
   } catch (const std::exception &e) {
     return fail(MSM_E_HIP, e.what());
@@ -672,6 +705,7 @@ int msm_ches_ctx_get_table(msm_ches_ctx *ctx, void *out, size_t first, size_t co
 int msm_ches_ctx_mult(msm_ches_ctx *ctx, void *ret, const byte *scalars, size_t stride, int on_device,
                       void *stream) {
   if (!ctx || !ret || stride < 32) return fail(MSM_E_ARG, "bad args (stride must be >= 32)");
+  if (!ctx->ready) return fail(MSM_E_STATE, "no table: build_table, set_table or load_table first");
   try {
     DeviceGuard g(ctx->device);
     hipStream_t s = (hipStream_t)stream;
@@ -700,6 +734,7 @@ int msm_ches_ctx_mult(msm_ches_ctx *ctx, void *ret, const byte *scalars, size_t 
 int msm_ches_ctx_mult_batch(msm_ches_ctx *ctx, void *rets, const byte *scalars, size_t stride, size_t set_stride,
                             size_t count, int on_device, void *stream) {
   if (!ctx || (!rets && count) || stride < 32) return fail(MSM_E_ARG, "bad args (stride must be >= 32)");
+  if (!ctx->ready) return fail(MSM_E_STATE, "no table: build_table, set_table or load_table first");
   try {
     DeviceGuard g(ctx->device);
     hipStream_t s = (hipStream_t)stream;
@@ -764,7 +799,9 @@ int msm_bgmw_ctx_create(msm_bgmw_ctx **ctx, int group, int device, int q_exp, in
 int msm_bgmw_ctx_build_table(msm_bgmw_ctx *ctx, const void *pts, size_t n, int on_device, void *stream) {
   if (!ctx || (!pts && n)) return fail(MSM_E_ARG, "bad args");
   try {
+    ctx->ready = false;
     CHES_DISPATCH(ctx, build_table(pts, n, on_device != 0, (hipStream_t)stream));
+    ctx->ready = true;
     return MSM_OK;
   } catch (const std::exception &e) {
     return fail(MSM_E_HIP, e.what());
@@ -774,7 +811,9 @@ int msm_bgmw_ctx_build_table(msm_bgmw_ctx *ctx, const void *pts, size_t n, int o
 int msm_bgmw_ctx_set_table(msm_bgmw_ctx *ctx, const void *tab, size_t n, int on_device, void *stream) {
   if (!ctx || (!tab && n)) return fail(MSM_E_ARG, "bad args");
   try {
+    ctx->ready = false;
     CHES_DISPATCH(ctx, set_table(tab, n, on_device != 0, (hipStream_t)stream));
+    ctx->ready = true;
     return MSM_OK;
   } catch (const std::exception &e) {
     return fail(MSM_E_HIP, e.what());
@@ -794,6 +833,7 @@ int msm_bgmw_ctx_get_table(msm_bgmw_ctx *ctx, void *out, size_t first, size_t co
 int msm_bgmw_ctx_mult(msm_bgmw_ctx *ctx, void *ret, const byte *scalars, size_t stride, int on_device,
                       void *stream) {
   if (!ctx || !ret || stride < 32) return fail(MSM_E_ARG, "bad args (stride must be >= 32)");
+  if (!ctx->ready) return fail(MSM_E_STATE, "no table: build_table, set_table or load_table first");
   try {
     DeviceGuard g(ctx->device);
     hipStream_t s = (hipStream_t)stream;
@@ -855,12 +895,12 @@ int msm_ches_ctx_load_table(msm_ches_ctx *ctx, const char *path) {
   if (!ctx || !path) return fail(MSM_E_ARG, "bad args");
   try {
     DeviceGuard g(ctx->device);
-    if (ctx->group == 1) {
-      const ChesParams &p = ctx->g1->params();
-      return load_table_file(*ctx->g1, 1, 1, p.q_exp, p.h, path);
-    }
-    const ChesParams &p = ctx->g2->params();
-    return load_table_file(*ctx->g2, 2, 1, p.q_exp, p.h, path);
+    ctx->ready = false;
+    const ChesParams &p = CHES_DISPATCH(ctx, params());
+    const int rc = ctx->group == 1 ? load_table_file(*ctx->g1, 1, 1, p.q_exp, p.h, path)
+                                   : load_table_file(*ctx->g2, 2, 1, p.q_exp, p.h, path);
+    ctx->ready = rc == MSM_OK;
+    return rc;
   } catch (const std::exception &e) {
     return fail(MSM_E_HIP, e.what());
   }
@@ -879,8 +919,11 @@ int msm_bgmw_ctx_load_table(msm_bgmw_ctx *ctx, const char *path) {
   if (!ctx || !path) return fail(MSM_E_ARG, "bad args");
   try {
     DeviceGuard g(ctx->device);
-    if (ctx->group == 1) return load_table_file(*ctx->g1, 1, 2, ctx->g1->q_exp(), ctx->g1->h(), path);
-    return load_table_file(*ctx->g2, 2, 2, ctx->g2->q_exp(), ctx->g2->h(), path);
+    ctx->ready = false;
+    const int rc = ctx->group == 1 ? load_table_file(*ctx->g1, 1, 2, ctx->g1->q_exp(), ctx->g1->h(), path)
+                                   : load_table_file(*ctx->g2, 2, 2, ctx->g2->q_exp(), ctx->g2->h(), path);
+    ctx->ready = rc == MSM_OK;
+    return rc;
   } catch (const std::exception &e) {
     return fail(MSM_E_HIP, e.what());
   }

@@ -352,7 +352,6 @@ Ches<G>::~Ches() {
   for (int k = 0; k < 2; ++k)
     if (tails_[k]) (void)hipStreamDestroy(tails_[k]);
   if (fstream_) (void)hipStreamDestroy(fstream_);
-  if (accs_) (void)hipStreamDestroy(accs_);
 }
 
 // bucket space = B plus (copies_ - 1) copies of the small buckets 1..small_;
@@ -553,14 +552,13 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *d_scalars, size_t stride, 
   if (!fstream_) {
     // the short digit/sort and latency-bound reduction kernels go ahead of the
     // long accumulation's pending workgroups: highest stream priority
+    // (measured alternatives -- tails at the lowest priority, accumulations on
+    // their own stream, front k+1 before head k -- were slower or equal)
     int least = 0, greatest = 0;
     MSM_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    const char *bm = std::getenv("MSM_BATCH_MODE");
-    bmode_ = bm ? std::atoi(bm) : 0;
     for (int k = 0; k < 2; ++k)
-      MSM_HIP_CHECK(hipStreamCreateWithPriority(&tails_[k], hipStreamNonBlocking, (bmode_ & 2) ? least : greatest));
+      MSM_HIP_CHECK(hipStreamCreateWithPriority(&tails_[k], hipStreamNonBlocking, greatest));
     MSM_HIP_CHECK(hipStreamCreateWithPriority(&fstream_, hipStreamNonBlocking, greatest));
-    if (bmode_ & 4) MSM_HIP_CHECK(hipStreamCreateWithPriority(&accs_, hipStreamNonBlocking, greatest));
     for (int k = 0; k < 2; ++k) {
       MSM_HIP_CHECK(hipEventCreateWithFlags(&ev_head_[k], hipEventDisableTiming));
       MSM_HIP_CHECK(hipEventCreateWithFlags(&ev_tail_[k], hipEventDisableTiming));
@@ -611,12 +609,9 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *d_scalars, size_t stride, 
     digits_sort(fstream_, d_scalars + k * set_stride, stride, (int)(k % kFronts));
     MSM_HIP_CHECK(hipEventRecord(evf[k], fstream_));
   };
-  hipStream_t as = accs_ ? accs_ : s;
-  if (accs_) MSM_HIP_CHECK(hipStreamWaitEvent(accs_, bev_[0], 0));
-  const bool front_first = bmode_ & 1;
-  if (front_first) issue_front(0);
+  hipStream_t as = s;
   for (size_t k = 0; k < count; ++k) {
-    if (!front_first) issue_front(k);
+    issue_front(k);
     const int set = (int)(k & 1), fset = (int)(k % kFronts);
     MSM_HIP_CHECK(hipStreamWaitEvent(as, evf[k], 0));
     if (k >= 2) MSM_HIP_CHECK(hipStreamWaitEvent(as, evh[k - 2], 0));  // bucket set free again
@@ -624,14 +619,7 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *d_scalars, size_t stride, 
     accumulate(as, fset, set);
     if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k + 1], as));
     MSM_HIP_CHECK(hipEventRecord(eva[k], as));
-    // front k+1 is issued before head k and head k waits for it: at the end of
-    // accumulation k both are ready, and a head dispatched first holds the
-    // dispatcher for its whole grid (~0.4 ms) while accumulation k+1 waits on
-    // its front (measured: profiles/r01f timeline).  Front first, then head k
-    // beside accumulation k+1.
-    if (front_first && k + 1 < count) issue_front(k + 1);
     MSM_HIP_CHECK(hipStreamWaitEvent(tails_[set], eva[k], 0));
-    if (front_first && k + 1 < count) MSM_HIP_CHECK(hipStreamWaitEvent(tails_[set], evf[k + 1], 0));
     red_.launch_head(tails_[set], buckets_[set].p, set);
     MSM_HIP_CHECK(hipEventRecord(evh[k], tails_[set]));
     red_.launch_tail(tails_[set], set, false);  // beside the accumulations: least resource time

@@ -27,11 +27,11 @@ struct Xyzz {
 };
 
 template <class F>
-__device__ __forceinline__ bool xyzz_is_inf(const Xyzz<F> &a) {
+MSM_FN bool xyzz_is_inf(const Xyzz<F> &a) {
   return f_is_zero_exact(a.zz);
 }
 template <class F>
-__device__ __forceinline__ void xyzz_set_inf(Xyzz<F> &a) {
+MSM_FN void xyzz_set_inf(Xyzz<F> &a) {
   f_zero(a.x);
   f_zero(a.y);
   f_zero(a.zzz);
@@ -40,7 +40,7 @@ __device__ __forceinline__ void xyzz_set_inf(Xyzz<F> &a) {
 // bucket := +-P   (ZZ = ZZZ = 1, Y negated instead of ZZZ; same point as the
 // reference's (X, Y, -1, 1) representative of ec_ops.h:720-724)
 template <class F>
-__device__ __forceinline__ void xyzz_from_aff(Xyzz<F> &r, const Aff<F> &p, bool neg) {
+MSM_FN void xyzz_from_aff(Xyzz<F> &r, const Aff<F> &p, bool neg) {
   r.x = p.x;
   if (neg) {
     f_neg4(r.y, p.y);
@@ -56,7 +56,7 @@ __device__ __forceinline__ void xyzz_from_aff(Xyzz<F> &r, const Aff<F> &p, bool 
 //   U = 2Y, V = U^2, W = U V, S = X V, M = 3 X^2 (+ a ZZ^2, a = 0)
 //   X3 = M^2 - 2S, Y3 = M (S - X3) - W Y, ZZ3 = V ZZ, ZZZ3 = W ZZZ
 template <class F>
-__device__ __forceinline__ void xyzz_dbl(Xyzz<F> &r, const Xyzz<F> &a) {
+MSM_FN void xyzz_dbl(Xyzz<F> &r, const Xyzz<F> &a) {
   if (xyzz_is_inf(a)) {
     r = a;
     return;
@@ -84,7 +84,7 @@ __device__ __forceinline__ void xyzz_dbl(Xyzz<F> &r, const Xyzz<F> &a) {
 // acc += (neg ? -P : P); P affine, canonical, not infinity (callers skip the
 // all-zero affine point, as ec_ops.h:717 does).
 template <class F>
-__device__ __forceinline__ void xyzz_madd(Xyzz<F> &acc, const Aff<F> &p, bool neg) {
+MSM_FN void xyzz_madd(Xyzz<F> &acc, const Aff<F> &p, bool neg) {
   if (xyzz_is_inf(acc)) {
     xyzz_from_aff(acc, p, neg);
     return;
@@ -135,7 +135,7 @@ __device__ __forceinline__ void xyzz_madd(Xyzz<F> &acc, const Aff<F> &p, bool ne
 
 // acc += b, both xyzz in S
 template <class F>
-__device__ __forceinline__ void xyzz_add(Xyzz<F> &acc, const Xyzz<F> &b) {
+MSM_FN void xyzz_add(Xyzz<F> &acc, const Xyzz<F> &b) {
   if (xyzz_is_inf(b)) return;
   if (xyzz_is_inf(acc)) {
     acc = b;

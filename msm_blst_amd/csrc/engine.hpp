@@ -255,8 +255,6 @@ class Ches {
   WeightedReducer<G> red_;
   std::vector<hipEvent_t> ev_;
   hipStream_t tails_[2] = {nullptr, nullptr}, fstream_ = nullptr;
-  hipStream_t accs_ = nullptr;  // MSM_BATCH_MODE bit 2: accumulations on a greatest-priority stream
-  int bmode_ = 0;  // batch issue order / tail priority (MSM_BATCH_MODE, read at stream creation)
   hipEvent_t ev_head_[2] = {nullptr, nullptr}, ev_tail_[2] = {nullptr, nullptr};
   hipEvent_t ev_front_[2] = {nullptr, nullptr}, ev_acc_[2] = {nullptr, nullptr};
   void *host_out_[2] = {nullptr, nullptr};

@@ -781,33 +781,38 @@ void or_bgmw_digits(int *d, const uint8_t *s32, int q_exp, int h) {
   qhalf_digits(d, t, q_exp, h);
   for (int j = 0; j < h; ++j) d[j] = -d[j];
 }
-void or_p1_bgmw_table(or_p1_affine *T, const or_p1_affine *P, size_t n, int q_exp, int h) {
-  size_t tot = n * (size_t)h;
-  or_p1 *J = (or_p1 *)malloc(sizeof(or_p1) * tot);
-  for (size_t i = 0; i < n; ++i) {
-    or_p1 Q; p1_from_affine(&Q, &P[i]);
-    for (int j = 0; j < h; ++j) {
-      J[i * (size_t)h + j] = Q;
-      for (int e = 0; e < q_exp; ++e) p1_dbl(&Q, &Q);
-    }
+#define DEFINE_BGMW(PT)                                                                                   \
+  /* T[i*h+j] = q^j*P_i (ref main_p1.cpp:94-122) */                                                      \
+  void or_##PT##_bgmw_table(or_##PT##_affine *T, const or_##PT##_affine *P, size_t n, int q_exp, int h) { \
+    size_t tot = n * (size_t)h;                                                                          \
+    or_##PT *J = (or_##PT *)malloc(sizeof(or_##PT) * tot);                                               \
+    for (size_t i = 0; i < n; ++i) {                                                                     \
+      or_##PT Q; PT##_from_affine(&Q, &P[i]);                                                            \
+      for (int j = 0; j < h; ++j) {                                                                      \
+        J[i * (size_t)h + j] = Q;                                                                        \
+        for (int e = 0; e < q_exp; ++e) PT##_dbl(&Q, &Q);                                                \
+      }                                                                                                  \
+    }                                                                                                    \
+    PT##s_to_aff(T, J, tot);                                                                             \
+    free(J);                                                                                             \
+  }                                                                                                      \
+  /* ref multi_scalar.c:506-547 + integrate_buckets :281-297 */                                          \
+  void or_##PT##_bgmw_msm(or_##PT *r, const or_##PT##_affine *T, size_t n, const uint8_t *s32, int q_exp, int h) { \
+    size_t nbk = (size_t)1 << (q_exp - 1);                                                               \
+    or_##PT##xyzz *bk = (or_##PT##xyzz *)calloc(nbk, sizeof(or_##PT##xyzz));                             \
+    int d[64];                                                                                           \
+    for (size_t i = 0; i < n; ++i) {                                                                     \
+      or_bgmw_digits(d, s32 + 32 * i, q_exp, h);                                                         \
+      for (int j = 0; j < h; ++j) {                                                                      \
+        if (d[j] > 0) PT##xyzz_madd(&bk[d[j] - 1], &bk[d[j] - 1], &T[i * (size_t)h + j], 0);            \
+        else if (d[j] < 0) PT##xyzz_madd(&bk[-d[j] - 1], &bk[-d[j] - 1], &T[i * (size_t)h + j], 1);     \
+      }                                                                                                  \
+    }                                                                                                    \
+    or_##PT##xyzz acc = bk[nbk - 1], sum = bk[nbk - 1];                                                  \
+    for (size_t k = nbk - 1; k-- > 0;) { PT##xyzz_add(&acc, &acc, &bk[k]); PT##xyzz_add(&sum, &sum, &acc); } \
+    PT##xyzz_to_j(r, &sum);                                                                              \
+    free(bk);                                                                                            \
   }
-  p1s_to_aff(T, J, tot);
-  free(J);
-}
-/* ref multi_scalar.c:506-547 + integrate_buckets :281-297 */
-void or_p1_bgmw_msm(or_p1 *r, const or_p1_affine *T, size_t n, const uint8_t *s32, int q_exp, int h) {
-  size_t nbk = (size_t)1 << (q_exp - 1);
-  or_p1xyzz *bk = (or_p1xyzz *)calloc(nbk, sizeof(or_p1xyzz));
-  int d[64];
-  for (size_t i = 0; i < n; ++i) {
-    or_bgmw_digits(d, s32 + 32 * i, q_exp, h);
-    for (int j = 0; j < h; ++j) {
-      if (d[j] > 0) p1xyzz_madd(&bk[d[j] - 1], &bk[d[j] - 1], &T[i * (size_t)h + j], 0);
-      else if (d[j] < 0) p1xyzz_madd(&bk[-d[j] - 1], &bk[-d[j] - 1], &T[i * (size_t)h + j], 1);
-    }
-  }
-  or_p1xyzz acc = bk[nbk - 1], sum = bk[nbk - 1];
-  for (size_t k = nbk - 1; k-- > 0;) { p1xyzz_add(&acc, &acc, &bk[k]); p1xyzz_add(&sum, &sum, &acc); }
-  p1xyzz_to_j(r, &sum);
-  free(bk);
-}
+
+DEFINE_BGMW(p1)
+DEFINE_BGMW(p2)

@@ -1,6 +1,7 @@
-// ref_driver_p1.cpp -- golden harness around the REFERENCE's own n=2^10 G1
-// driver (main_p1.cpp compiled where it lies, main() renamed; its
-// config_file.h is config_file_n_exp_10.h: q=2^13, h=20, |B|=1725).
+// ref_driver.cpp -- golden harness around the REFERENCE's own n=2^10 G1 / G2
+// drivers (main_p1.cpp / main_p2.cpp compiled where they lie, main() renamed;
+// their config_file.h is config_file_n_exp_10.h: q=2^13, h=20, |B|=1725).
+// -DGROUP=1 (default) or -DGROUP=2 selects the driver it is linked against.
 //
 // Calls the reference's init_fix_point_list / init_pippenger_CHES_q_over_5 /
 // init_pippenger_BGMW95 and its four timed methods on SplitMix64-seeded
@@ -9,7 +10,8 @@
 // q/2 digits of the first scalars, and the compressed result of every method
 // for seeds 1..3 plus the crafted scalar that trips the CHES last-element
 // guard (SURVEY 8a defect 1).  Test infrastructure only; output is committed
-// as tests/golden/ches_driver_n10.json by tests/golden/make_golden.py.
+// as tests/golden/ches_driver_n10.json (G1) / ches_driver_p2_n10.json (G2) by
+// tests/golden/make_golden.py.
 #include <array>
 #include <cstdint>
 #include <cstdio>
@@ -18,20 +20,30 @@
 #include "bindings/blst.h"
 #include "src_from_aztec/numeric/uint256/uint256.hpp"
 
+#ifndef GROUP
+#define GROUP 1
+#endif
+#if GROUP == 1
+typedef blst_p1_affine Paff;
+#define PAFF_COMPRESS blst_p1_affine_compress
+#else
+typedef blst_p2_affine Paff;
+#define PAFF_COMPRESS blst_p2_affine_compress
+#endif
 constexpr int H = 20, HB = 22, Q = 1 << 13, N = 1 << 10, BSZ = 1725;
 
 extern digit_decomposition *DIGIT_CONVERSION_HASH_TABLE;
 extern int *BUCKET_SET;
-extern blst_p1_affine *FIX_POINTS_LIST;
-extern blst_p1_affine *PRECOMPUTATION_POINTS_LIST_3nh;
-extern blst_p1_affine *PRECOMPUTATION_POINTS_LIST_BGMW95;
+extern Paff *FIX_POINTS_LIST;
+extern Paff *PRECOMPUTATION_POINTS_LIST_3nh;
+extern Paff *PRECOMPUTATION_POINTS_LIST_BGMW95;
 void init_fix_point_list();
 void init_pippenger_CHES_q_over_5();
 void init_pippenger_BGMW95();
-blst_p1_affine pippenger_variant_q_over_5_CHES(uint256_t scalars_array[]);
-blst_p1_affine pippenger_variant_q_over_5_CHES_integral_scalar_conversion(uint256_t scalars_array[]);
-blst_p1_affine pippenger_variant_BGMW95(uint256_t scalars_array[]);
-blst_p1_affine pippenger_blst_built_in(uint256_t scalars_array[]);
+Paff pippenger_variant_q_over_5_CHES(uint256_t scalars_array[]);
+Paff pippenger_variant_q_over_5_CHES_integral_scalar_conversion(uint256_t scalars_array[]);
+Paff pippenger_variant_BGMW95(uint256_t scalars_array[]);
+Paff pippenger_blst_built_in(uint256_t scalars_array[]);
 void trans_uint256_t_to_MB_radixq_expr(std::array<std::array<int, 2>, H> &ret, const uint256_t &a);
 void trans_uint256_t_to_qhalf_expr(std::array<int, HB> &ret, const uint256_t &a);
 
@@ -68,17 +80,17 @@ static uint64_t fnv(const void *p, size_t len) {
   return h;
 }
 static void phex(const uint8_t *b, size_t n) { for (size_t i = 0; i < n; ++i) printf("%02x", b[i]); }
-static void pres(const char *k, const blst_p1_affine &a) {
-  uint8_t o[48];
-  blst_p1_affine_compress(o, &a);
-  printf("\"%s\": \"", k); phex(o, 48); printf("\"");
+static void pres(const char *k, const Paff &a) {
+  uint8_t o[48 * GROUP];
+  PAFF_COMPRESS(o, &a);
+  printf("\"%s\": \"", k); phex(o, 48 * GROUP); printf("\"");
 }
 
 int main() {
   init_fix_point_list();
   init_pippenger_CHES_q_over_5();
   init_pippenger_BGMW95();
-  printf("{\"n\": %d, \"q_exp\": 13, \"h\": %d, \"b_size\": %d, \"q_exp_bgmw\": 12, \"h_bgmw\": %d,\n", N, H, BSZ, HB);
+  printf("{\"group\": %d, \"n\": %d, \"q_exp\": 13, \"h\": %d, \"b_size\": %d, \"q_exp_bgmw\": 12, \"h_bgmw\": %d,\n", GROUP, N, H, BSZ, HB);
   printf("\"bucket_set\": [");
   for (int i = 0; i < BSZ; ++i) printf("%s%d", i ? "," : "", BUCKET_SET[i]);
   printf("],\n\"digit_table\": [");
@@ -87,11 +99,11 @@ int main() {
     printf("%s[%d,%d,%d]", v ? "," : "", t.m, t.b, t.alpha);
   }
   printf("],\n");
-  printf("\"fnv_fixed_points\": \"%016llx\",\n", (unsigned long long)fnv(FIX_POINTS_LIST, sizeof(blst_p1_affine) * N));
+  printf("\"fnv_fixed_points\": \"%016llx\",\n", (unsigned long long)fnv(FIX_POINTS_LIST, sizeof(Paff) * N));
   printf("\"fnv_table_3nh\": \"%016llx\",\n",
-         (unsigned long long)fnv(PRECOMPUTATION_POINTS_LIST_3nh, sizeof(blst_p1_affine) * 3 * N * H));
+         (unsigned long long)fnv(PRECOMPUTATION_POINTS_LIST_3nh, sizeof(Paff) * 3 * N * H));
   printf("\"fnv_table_bgmw\": \"%016llx\",\n",
-         (unsigned long long)fnv(PRECOMPUTATION_POINTS_LIST_BGMW95, sizeof(blst_p1_affine) * N * HB));
+         (unsigned long long)fnv(PRECOMPUTATION_POINTS_LIST_BGMW95, sizeof(Paff) * N * HB));
   static uint256_t sc[N];
   printf("\"runs\": [\n");
   for (int seed = 1; seed <= 4; ++seed) {

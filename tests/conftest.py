@@ -27,3 +27,19 @@ def golden():
             return json.load(f)
 
     return load
+
+
+_POINTS = {}
+
+
+@pytest.fixture(scope="session")
+def points():
+    """fixed_points(group, n) of the engine's host helper, cached for the session
+    (G2 n = 2^20 takes seconds on the host and is used by several modules)."""
+    def get(group, n):
+        key = (group, n)
+        if key not in _POINTS:
+            import msm_blst_amd as m
+            _POINTS[key] = m.fixed_points(group, n)
+        return _POINTS[key]
+    return get

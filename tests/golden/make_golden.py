@@ -16,6 +16,7 @@ Fixtures written:
   xyzz_kat.json              blst_p1xyzz_dadd_affine / _dadd sequences (raw limbs + compressed)
   ches_driver_n10.json       the reference's own n=2^10 G1 driver: bucket set, digit
                              table, table hashes, digits, results of all 4 methods
+  ches_driver_p2_n10.json    the same for the reference's G2 driver (main_p2.cpp)
   ches_params_n{10,16,20}.json  bucket set / digit table hashes + MB / q/2 digits
   ches_configs.json          the 17 ches_config_files/*.h parameter sets (values)
 """
@@ -93,10 +94,7 @@ def main():
         rows.append({"ops": ops, "x": x, "y": y, "zzz": zzz, "zz": zz, "compressed": c1, "compressed_double": c2})
     json.dump({"source": "reference blst_p1xyzz_dadd_affine sequences on P_0..P_2, then acc+acc via blst_p1xyzz_dadd",
                "sequences": rows}, open(os.path.join(HERE, "xyzz_kat.json"), "w"), indent=1)
-    s = run([os.path.join(BIN, "ref_driver_p1")])
-    d = json.loads(s[s.index('{"n"'):])
-    d["source"] = "reference main_p1.cpp (config_file.h = n_exp_10) via oracle/ref_driver_p1.cpp"
-    json.dump(d, open(os.path.join(HERE, "ches_driver_n10.json"), "w"))
+    drivers()
     for c in (10, 16, 20):
         d = json.loads(run([os.path.join(BIN, f"ref_ches_{c}")]))
         d["source"] = f"reference auxiliaryfunc.h under config_file_n_exp_{c}.h via oracle/ref_ches_params.cpp"
@@ -117,5 +115,19 @@ def main():
               open(os.path.join(HERE, "ches_configs.json"), "w"), indent=1)
 
 
+def drivers():
+    """The reference's own n=2^10 drivers (main_p1.cpp -> ches_driver_n10.json,
+    main_p2.cpp -> ches_driver_p2_n10.json) through oracle/ref_driver.cpp."""
+    for g, fname in ((1, "ches_driver_n10.json"), (2, "ches_driver_p2_n10.json")):
+        s = run([os.path.join(BIN, f"ref_driver_p{g}")])
+        d = json.loads(s[s.index('{"group"'):])
+        d["source"] = f"reference main_p{g}.cpp (config_file.h = n_exp_10) via oracle/ref_driver.cpp (GROUP={g})"
+        json.dump(d, open(os.path.join(HERE, fname), "w"))
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["drivers"]:
+        subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "ref", f"REF={REF}"], check=True)
+        drivers()
+    else:
+        main()

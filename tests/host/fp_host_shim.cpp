@@ -1,0 +1,93 @@
+// fp_host_shim.cpp -- host (g++) build of the engine's field and xyzz headers
+// (msm_blst_amd/csrc/fp.hpp, ec.hpp) with every range check enabled
+// (MSM_FP_HOST_TEST: a wrapping 64-bit column, a wrapping or negative limb, or
+// a negative reduced value sets msm_fp_overflow).  TEST INFRASTRUCTURE ONLY:
+// loaded by tests/test_fp_bounds.py through ctypes; the same header text is
+// compiled for gfx950 in the product.
+#define MSM_FP_HOST_TEST 1
+#include <string.h>
+
+#include "../../msm_blst_amd/csrc/ec.hpp"
+
+extern "C" {
+int msm_fp_overflow = 0;
+
+using namespace msm;
+
+static Fp ld(const uint32_t *p) {
+  Fp r;
+  memcpy(r.v, p, sizeof r.v);
+  return r;
+}
+static void st(uint32_t *p, const Fp &a) { memcpy(p, a.v, sizeof a.v); }
+static Fp2 ld2(const uint32_t *p) { return Fp2{ld(p), ld(p + NL)}; }
+static void st2(uint32_t *p, const Fp2 &a) {
+  st(p, a.c0);
+  st(p + NL, a.c1);
+}
+
+int h_overflow(int clear) {
+  int v = msm_fp_overflow;
+  if (clear) msm_fp_overflow = 0;
+  return v;
+}
+
+// ---- Fp primitives (op codes as in tests/test_fp_bounds.py) ----
+void h_fp_op(int op, uint32_t *r, const uint32_t *a, const uint32_t *b, const uint32_t *c, const uint32_t *d,
+             const uint32_t *e, const uint32_t *f, const uint32_t *g, const uint32_t *h) {
+  Fp R;
+  switch (op) {
+    case 0: fp_mul(R, ld(a), ld(b)); break;
+    case 1: fp_sqr(R, ld(a)); break;
+    case 2: fp_mul2(R, ld(a), ld(b), ld(c), ld(d)); break;
+    case 3: fp_mul4(R, ld(a), ld(b), ld(c), ld(d), ld(e), ld(f), ld(g), ld(h)); break;
+    case 4: R = ld(a); fp_red(R); break;
+    case 5: R = ld(a); fp_nred(R); break;
+    case 6: fp_sub<4>(R, ld(a), ld(b)); break;
+    case 7: fp_sub<8>(R, ld(a), ld(b)); break;
+    case 8: fp_sub<32>(R, ld(a), ld(b)); break;
+    case 9: f_mul_sub(R, ld(a), ld(b), ld(c), ld(d)); break;
+    default: return;
+  }
+  st(r, R);
+}
+// ---- Fp2 (components c0 | c1, 28 words) ----
+void h_fp2_op(int op, uint32_t *r, const uint32_t *a, const uint32_t *b, const uint32_t *c, const uint32_t *d) {
+  Fp2 R;
+  switch (op) {
+    case 0: f_mul(R, ld2(a), ld2(b)); break;
+    case 1: f_sqr(R, ld2(a)); break;
+    case 2: f_mul_bs(R, ld2(a), ld2(b)); break;
+    case 3: f_mul_sub(R, ld2(a), ld2(b), ld2(c), ld2(d)); break;
+    default: return;
+  }
+  st2(r, R);
+}
+
+}  // extern "C"
+
+// ---- xyzz formulas: op 0 madd(acc, P, neg), 1 add(acc, B), 2 dbl(acc) ----
+template <class F>
+static void xyzz_io(int op, uint32_t *acc, const uint32_t *other, int neg) {
+  constexpr int W = sizeof(F) / 4;
+  Xyzz<F> A;
+  memcpy(&A, acc, sizeof A);
+  if (op == 0) {
+    Aff<F> p;
+    memcpy(&p, other, sizeof p);
+    xyzz_madd(A, p, neg != 0);
+  } else if (op == 1) {
+    Xyzz<F> B;
+    memcpy(&B, other, sizeof B);
+    xyzz_add(A, B);
+  } else {
+    Xyzz<F> t = A;
+    xyzz_dbl(A, t);
+  }
+  memcpy(acc, &A, sizeof A);
+  (void)W;
+}
+extern "C" void h_xyzz(int group, int op, uint32_t *acc, const uint32_t *other, int neg) {
+  if (group == 1) xyzz_io<Fp>(op, acc, other, neg);
+  else xyzz_io<Fp2>(op, acc, other, neg);
+}

@@ -49,13 +49,14 @@ def lib():
         L.or_ches_digit_table.argtypes = [vp, vp, vp, sz, ctypes.c_int]
         L.or_ches_mb_digits.argtypes = [vp, vp, vp, vp, vp, ctypes.c_int, ctypes.c_int]
         L.or_ches_params_for.argtypes = [ctypes.c_int, ctypes.c_int, vp]
-        for f in ("or_p1_ches_table", "or_p2_ches_table", "or_p1_bgmw_table"):
+        for f in ("or_p1_ches_table", "or_p2_ches_table", "or_p1_bgmw_table", "or_p2_bgmw_table"):
             getattr(L, f).argtypes = [vp, vp, sz, ctypes.c_int, ctypes.c_int]
         for f in ("or_p1_ches_msm", "or_p2_ches_msm"):
             getattr(L, f).argtypes = [vp, vp, sz, vp, vp, vp, vp, sz, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.or_p1_ches_reduce.argtypes = [vp, vp, vp, sz, ctypes.c_int]
         L.or_bgmw_digits.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int]
-        L.or_p1_bgmw_msm.argtypes = [vp, vp, sz, vp, ctypes.c_int, ctypes.c_int]
+        for f in ("or_p1_bgmw_msm", "or_p2_bgmw_msm"):
+            getattr(L, f).argtypes = [vp, vp, sz, vp, ctypes.c_int, ctypes.c_int]
         _lib = L
     return _lib
 

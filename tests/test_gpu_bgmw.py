@@ -76,19 +76,19 @@ def test_edge_scalars_n10(m, ctx10, golden):
 
 
 @pytest.mark.parametrize("n_exp", [16, 20])
-def test_bgmw_g1_large_vs_reference(m, golden, n_exp):
+def test_bgmw_g1_large_vs_reference(m, golden, points, n_exp):
     n = 1 << n_exp
     ctx = m.BGMWContext(1, 0, n_exp=n_exp)
-    ctx.build_table(m.fixed_points(1, n), n)
+    ctx.build_table(points(1, n), n)
     assert m.compress(1, ctx.mult(bytes(m.gen_scalars(n, 1)))).hex() == _golden(golden, 1, n)
     ctx.close()
 
 
-@pytest.mark.parametrize("n_exp", [10, 16])
-def test_bgmw_g2_vs_reference(m, golden, n_exp):
+@pytest.mark.parametrize("n_exp", [10, 16, 20])
+def test_bgmw_g2_vs_reference(m, golden, points, n_exp):
     n = 1 << n_exp
     ctx = m.BGMWContext(2, 0, n_exp=n_exp)
-    ctx.build_table(m.fixed_points(2, n), n)
+    ctx.build_table(points(2, n), n)
     assert m.compress(2, ctx.mult(bytes(m.gen_scalars(n, 1)))).hex() == _golden(golden, 2, n)
     ctx.close()
 

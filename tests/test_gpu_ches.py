@@ -96,10 +96,10 @@ def test_equal_points_doubling_branch(m):
 
 
 @pytest.mark.parametrize("n_exp", [16, 20])
-def test_ches_g1_large_vs_reference(m, golden, n_exp):
+def test_ches_g1_large_vs_reference(m, golden, points, n_exp):
     n = 1 << n_exp
     ctx = m.CHESContext(1, 0, n_exp=n_exp)
-    ctx.build_table(m.fixed_points(1, n), n)
+    ctx.build_table(points(1, n), n)
     r = ctx.mult(m.gen_scalars(n, 1))
     assert m.compress(1, r).hex() == _golden(golden, 1, n)
     # buffers reused; the atomics-ordered accumulation may pick another Jacobian
@@ -108,11 +108,12 @@ def test_ches_g1_large_vs_reference(m, golden, n_exp):
     ctx.close()
 
 
-@pytest.mark.parametrize("n_exp", [10, 16])
-def test_ches_g2_vs_reference(m, golden, n_exp):
+@pytest.mark.parametrize("n_exp", [10, 16, 20])
+def test_ches_g2_vs_reference(m, golden, points, n_exp):
+    """G2 CHES incl. configs[4] (n = 2^20: q = 2^22, h = 12, table 9.7 GB in HBM)"""
     n = 1 << n_exp
     ctx = m.CHESContext(2, 0, n_exp=n_exp)
-    ctx.build_table(m.fixed_points(2, n), n)
+    ctx.build_table(points(2, n), n)
     r = ctx.mult(m.gen_scalars(n, 1))
     assert m.compress(2, r).hex() == _golden(golden, 2, n)
     ctx.close()

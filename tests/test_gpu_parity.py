@@ -135,11 +135,12 @@ def test_msm_ctx_window_sweep(L, golden):
         ctx.close()
 
 
-@pytest.mark.parametrize("group,n", [(1, 1 << 16), (1, 1 << 20), (2, 1 << 16)])
-def test_msm_large_vs_reference(L, golden, group, n):
+@pytest.mark.parametrize("group,n", [(1, 1 << 16), (1, 1 << 20), (2, 1 << 16), (2, 1 << 20)])
+def test_msm_large_vs_reference(L, golden, points, group, n):
+    """configs[1] (G1 2^16) and configs[4] (G2 2^20, the Fp2 path) by plain Pippenger"""
     import msm_blst_amd as m
     want = [c for c in golden(f"msm_g{group}.json")["cases"] if c["n"] == n and c["seed"] == 1][0]["compressed"]
-    pts = m.fixed_points(group, n)
+    pts = points(group, n)
     sc = m.gen_scalars(n, 1)
     ctx = m.MSMContext(group, 0, 16 if n >= (1 << 18) else 13)
     ctx.set_points(pts, n)

@@ -93,3 +93,55 @@ def test_points_add_pointer_rule_and_infinity(m):
     # all infinity -> infinity
     Z = (ctypes.c_uint8 * (96 * 8))()
     assert m.compress(1, m.ps_add(1, Z, 8)).hex() == "c0" + "00" * 47
+
+
+@pytest.mark.parametrize("kind", ["ches", "bgmw"])
+def test_table_file_truncated_or_padded_is_rejected(m, golden, tmp_path, kind):
+    """A file whose size disagrees with its header is refused before the context is
+    touched; a context whose load failed has no table and its mult raises
+    (MSM_E_STATE) instead of returning a point."""
+    n = 256
+    Ctx = m.CHESContext if kind == "ches" else m.BGMWContext
+    a = Ctx(1, 0, n_exp=10)
+    a.build_table(m.fixed_points(1, n), n)
+    good = tmp_path / "good.tbl"
+    a.save_table(good)
+    raw = good.read_bytes()
+    sc = bytes(m.gen_scalars(n, 1))
+    want = m.compress(1, a.mult(sc))
+    for name, data in (("short", raw[:-96]), ("long", raw + bytes(96)), ("header_only", raw[:64])):
+        bad = tmp_path / f"{name}.tbl"
+        bad.write_bytes(data)
+        b = Ctx(1, 0, n_exp=10)
+        with pytest.raises(m.MsmError):
+            b.load_table(bad)
+        with pytest.raises(m.MsmError):
+            b.mult(sc)
+        # a context with a valid table keeps it usable after a rejected load? No:
+        # a failed load leaves no table (never a half-loaded one) -> mult raises
+        b.load_table(good)
+        assert m.compress(1, b.mult(sc)) == want
+        with pytest.raises(m.MsmError):
+            b.load_table(bad)
+        with pytest.raises(m.MsmError):
+            b.mult(sc)
+        b.close()
+    # header with a row count that disagrees with its point count
+    hdr = bytearray(raw[:64])
+    hdr[32:40] = (int.from_bytes(hdr[32:40], "little") + 1).to_bytes(8, "little")
+    bad = tmp_path / "rows.tbl"
+    bad.write_bytes(bytes(hdr) + raw[64:])
+    b = Ctx(1, 0, n_exp=10)
+    with pytest.raises(m.MsmError):
+        b.load_table(bad)
+    b.close()
+    a.close()
+
+
+@pytest.mark.parametrize("kind", ["ches", "bgmw"])
+def test_mult_without_table_raises(m, kind):
+    Ctx = m.CHESContext if kind == "ches" else m.BGMWContext
+    c = Ctx(1, 0, n_exp=10)
+    with pytest.raises(m.MsmError):
+        c.mult(bytes(32 * 4))
+    c.close()

@@ -256,3 +256,38 @@ def test_ches_driver_results(ches_n10):
             sg = (ctypes.c_uint8 * h)()
             of.lib().or_ches_mb_digits(b, sg, m, ctypes.byref(sc, 32 * i), H, qe, h)
             assert [[(-m[j] if sg[j] else m[j]), b[j]] for j in range(h)] == run["mb_digits"][k]
+
+
+def test_ches_driver_p2_n10(golden):
+    """The oracle's G2 CHES / BGMW95 tables and methods against the reference's own G2
+    driver (main_p2.cpp, n = 2^10); its Pippenger results equal msm_g2.json."""
+    g = golden("ches_driver_p2_n10.json")
+    n, h, qe, qb, hb = g["n"], g["h"], g["q_exp"], g["q_exp_bgmw"], g["h_bgmw"]
+    assert g["group"] == 2
+    B = of.bucket_set(1 << qe, 231)
+    assert list(B) == g["bucket_set"]
+    H, v2i = of.digit_table(B, 1 << qe)
+    P = of.fixed_points(2, n)
+    assert _fnv(bytes(P)) == g["fnv_fixed_points"]
+    T = of.buf(192 * 3 * n * h)
+    of.lib().or_p2_ches_table(T, P, n, qe, h)
+    assert _fnv(bytes(T)) == g["fnv_table_3nh"]
+    TB = of.buf(192 * n * hb)
+    of.lib().or_p2_bgmw_table(TB, P, n, qb, hb)
+    assert _fnv(bytes(TB)) == g["fnv_table_bgmw"]
+    gold = {(c["seed"]): c["compressed"] for c in golden("msm_g2.json")["cases"]
+            if c["n"] == n and c["case"] == "rand" and c["nbits"] == 255}
+    for run in g["runs"]:
+        if run["case"] != "rand":
+            assert run["ches_q_over_5"] != run["pippenger"]  # the last-element guard defect, G2 too
+            continue
+        assert run["ches_q_over_5"] == run["ches_integral"] == run["bgmw95"] == run["pippenger"]
+        if run["seed"] in gold:
+            assert run["pippenger"] == gold[run["seed"]]
+        if run["seed"] == 1:  # oracle methods (G2 is slow on the CPU: one seed)
+            sc = of.scalars(n, 1)
+            r = of.buf(288)
+            of.lib().or_p2_ches_msm(r, T, n, sc, H, v2i, B, len(B), qe, h, 6)
+            assert of.compress(2, r) == run["pippenger"]
+            of.lib().or_p2_bgmw_msm(r, TB, n, sc, qb, hb)
+            assert of.compress(2, r) == run["pippenger"]
