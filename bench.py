@@ -1,28 +1,38 @@
 #!/usr/bin/env python3
 """bench.py -- G1 MSM point-scalar pairs/s at n=2^20 per MI355X (BASELINE.json metric).
 
-One step = one complete G1 MSM over this rank's 2^20 fixed points with the
-scalars already resident in HBM, by the reference's CHES "nh + q/5" method
-(BASELINE.json configs[2]: q = 2^22, h = 12, |B| = 874 437, precomputed table
-T = m q^j P_i resident in HBM): MB digit conversion -> bucket sort -> bucket
-accumulation -> weighted bucket reduction, plus, for N > 1, the single exchange
-of the partial sums (all_gather of 144-B Jacobians over RCCL) and their fold.
-The plain Pippenger path (configs[1] method) is timed beside it (`methods`).
-Weak scaling: every GPU owns its own 2^20-point shard of the sequence
-P_i = 2^(i+1) G, so the job computes an MSM of N * 2^20 pairs per step.
+One step = one complete G1 MSM over this rank's 2^20 fixed points by the
+reference's CHES "nh + q/5" method (BASELINE.json configs[2]: q = 2^22, h = 12,
+|B| = 874 437, precomputed table T = m q^j P_i resident in HBM), with its own
+scalar set: MB digit conversion -> bucket sort -> bucket accumulation ->
+weighted bucket reduction, plus, for N > 1, the single exchange of the partial
+sums (all_gather of 144-B Jacobians over RCCL) and their fold.
+
+Headline `value` ("scalars H2D included"): the K steps are K MSMs
+over K DISTINCT scalar sets that start in page-locked host memory; each set's
+32-MiB H2D copy is inside the timed region, issued by the pipelined batch
+(msm_ches_ctx_mult_batch) on its front stream so it overlaps earlier MSMs'
+accumulations.  Reported beside it: the same batch with the scalar sets already
+resident in HBM (`methods.ches_batch_resident`), K synchronous MSMs
+(`methods.ches_sync`), and the reference's other methods on the same points
+(plain Pippenger = configs[1] method, BGMW95).
+
+Parity (bit-exact): set 0 is the seed-1 scalar stream of BASELINE.md sec.3
+(rank r takes slice r of the N*2^20 stream), so the folded set-0 result is the
+golden MSM of N*2^20 points when tests/golden holds it; every batch result must
+equal the synchronous MSM of the same set; the last set is recomputed by the
+reference's own multi-threaded CPU grid (cpu_baseline); for N > 1 without a
+golden value each rank's set-0 partial is cross-checked with plain Pippenger.
+
+Weak scaling: every GPU owns its own 2^log_n-point shard of P_i = 2^(i+1) G.
+configs[3] (2^21 points over 8 GPUs): --log-n 18 --gpus 8.
 
 Usage:
   python bench.py [--gpus N --steps K --warmup W]                 (N = 1)
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
-
-Prints ONE JSON line on rank 0 with value = total pairs / (max-over-ranks
-time of K steps), a `roofline` object for the dominant kernel (bucket
-accumulation, timed with HIP events on the stream it runs on), and a
-`cpu_baseline` object (the reference's own blst_p1s_mult_pippenger built from
-/root/reference into oracle/_ref, 1 thread, on the same points and scalars;
-rank 0, N = 1 only; the oracle port if that build is absent).
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -34,72 +44,70 @@ sys.path.insert(0, REPO)
 METRIC = "G1 MSM point-scalar pairs/sec at n=2^20, 1/2/4/8 MI355X; bit-exact vs CPU"
 METRIC_G2 = "G2 MSM point-scalar pairs/sec at n=2^20 (BASELINE configs[4]); bit-exact vs CPU"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
-VALU_PEAK_LANE_OPS = 78.6e12   # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (one VALU op / lane / clk)
 MADS_PER_FPMUL = 392           # 14x14 product + 14x14 reduction, one v_mad_u64_u32 each (fp.hpp)
-FPMUL_PEAK = 76.8e9            # measured register-resident Fp-mul/s, tools/microbench/fp_rate.hip (profiles/)
+FPMUL_PEAK = 76.8e9            # measured register-resident Fp-mul/s: profiles/r02_fp_rate.txt (tools/microbench/fp_rate.hip)
 AFFINE_BYTES = 96              # one G1 affine point (blst layout), SURVEY 8d
 FPMUL_PER_MADD = 10            # 8M + 2S (ec_ops.h:727-748)
+CPU_THREADS = 16               # the GPU box's CPU share per GPU (16 threads)
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def timed_steps(step, ctx, steps, warmup, world, dev):
-    """W untimed + K timed steps bracketed by barrier + synchronize; max over ranks."""
-    import torch
-    for _ in range(warmup):
-        res = step()
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize(dev)
-    acc_ms, tot_ms = [], []
-    t_start = time.perf_counter()
-    for _ in range(steps):
-        res = step()
-        ph = ctx.phase_times()
-        acc_ms.append(ph["accumulate"])
-        tot_ms.append(ph["total"])
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        torch.distributed.barrier()
-    elapsed = time.perf_counter() - t_start
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
-    return res, elapsed, acc_ms, tot_ms, ctx.phase_times()
+class Bracket:
+    """W untimed warmup already done by the caller; barrier + synchronize on both
+    sides of the timed region, max over ranks."""
+
+    def __init__(self, world, dev):
+        self.world, self.dev = world, dev
+
+    def __enter__(self):
+        import torch
+        if self.world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize(self.dev)
+        self.t = time.perf_counter()
+        return self
+
+    def __exit__(self, *exc):
+        import torch
+        torch.cuda.synchronize(self.dev)
+        if self.world > 1:
+            torch.distributed.barrier()
+        el = time.perf_counter() - self.t
+        if self.world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=self.dev)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            el = float(t.item())
+        self.elapsed = el
+        return False
 
 
-def timed_batch(ctx, steps, warmup, world, dev, add):
-    """CHES batch mode: the K steps are K MSMs issued as one pipelined batch
-    (msm_ches_ctx_mult_batch: MSM k's bucket-reduction tail overlaps MSM k+1);
-    for N > 1 each step's partial is then exchanged and folded.  Same bracketing
-    (barrier + synchronize, max over ranks) as timed_steps."""
+def all_true(flag, world, dev):
+    """Logical AND of a per-rank boolean (None counts as unknown -> None)."""
+    if world == 1:
+        return flag
     import torch
-    from msm_blst_amd import dist as mdist
-    if warmup:
-        ctx._bench_batch(warmup)
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize(dev)
-    ctx.set_profiling(True)
-    t_start = time.perf_counter()
-    parts = ctx._bench_batch(steps)
-    if world > 1:
-        res = [mdist.fold(mdist.gather_partials(p, ctx.group, dev), add) for p in parts][-1]
-    else:
-        res = parts[-1]
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        torch.distributed.barrier()
-    elapsed = time.perf_counter() - t_start
-    acc_ms = [ctx.phase_times()["accumulate"]]
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
-    return res, elapsed, acc_ms
+    v = torch.tensor([-1 if flag is None else int(bool(flag))], dtype=torch.int32, device=dev)
+    torch.distributed.all_reduce(v, op=torch.distributed.ReduceOp.MIN)
+    x = int(v.item())
+    return None if x < 0 else bool(x)
+
+
+def make_scalar_sets(m, n, K, rank, world):
+    """K scalar sets of n 32-byte scalars in one page-locked host tensor.
+    Set 0: slice `rank` of the seed-1 stream of world*n scalars (golden key);
+    set k >= 1: its own seed per (k, rank)."""
+    import numpy as np
+    import torch
+    host = torch.empty(K * n * 32, dtype=torch.uint8, pin_memory=True)
+    hv = host.numpy()
+    s0 = m.gen_scalars(world * n, 1)
+    hv[:n * 32] = np.frombuffer(s0, dtype=np.uint8)[rank * n * 32:(rank + 1) * n * 32]
+    for k in range(1, K):
+        hv[k * n * 32:(k + 1) * n * 32] = np.frombuffer(m.gen_scalars(n, 1000 * k + rank + 1), dtype=np.uint8)
+    return host
 
 
 def main():
@@ -112,7 +120,7 @@ def main():
     ap.add_argument("--group", type=int, choices=(1, 2), default=1,
                     help="1: G1 (the BASELINE metric); 2: G2 (configs[4], Fp2 tower), reported under its own metric")
     ap.add_argument("--window", type=int, default=16, help="plain Pippenger window bits")
-    ap.add_argument("--no-compare", action="store_true", help="skip timing the other method (N = 1)")
+    ap.add_argument("--no-compare", action="store_true", help="skip the resident/sync/other-method legs")
     ap.add_argument("--no-batch", action="store_true",
                     help="CHES: time K independent synchronous MSMs instead of one pipelined batch of K")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -133,107 +141,149 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
 
-    from msm_blst_amd import _ffi
-    if not os.path.exists(_ffi.LIB_PATH):
-        from msm_blst_amd import build
-        build.build()
     import msm_blst_amd as m
     from msm_blst_amd import dist as mdist
+    m.lib()  # fails loudly when the HIP library is missing (build() first)
 
-    n = 1 << args.log_n
+    n, G, K, W = 1 << args.log_n, args.group, args.steps, args.warmup
     t0 = time.time()
     start, _ = mdist.shard_range(n * world, world, rank)
-    G = args.group
     pts = m.fixed_points(G, n, start)
-    sc = m.gen_scalars(n, 1 + rank)
-    log(f"[rank {rank}] inputs generated in {time.time() - t0:.1f}s (points {start}..{start + n})")
+    host = make_scalar_sets(m, n, K, rank, world)
+    log(f"[rank {rank}] inputs generated in {time.time() - t0:.1f}s (points {start}..{start + n}, {K} scalar sets)")
     stream = torch.cuda.current_stream(dev)
-    d_sc = torch.frombuffer(bytearray(bytes(sc)), dtype=torch.uint8).to(dev)
+    sp = stream.cuda_stream
+    d_all = host.to(dev)  # the same K sets resident in HBM (resident / sync legs)
+    hptr, dptr, SS = host.data_ptr(), d_all.data_ptr(), n * 32
     add = mdist.engine_add(G)
+
+    def keys(jacs):  # canonical comparison key: the compressed affine point (Jacobians differ in representative)
+        return [m.compress(G, j) for j in jacs]
+
+    def fold_all(parts):
+        if world == 1:
+            return parts
+        return [mdist.fold(ps, add) for ps in mdist.gather_partials_batch(parts, G, dev)]
 
     def make(method):
         t = time.time()
         if method == "ches":
             ctx = m.CHESContext(G, local, n_exp=args.log_n)
-            ctx.build_table(pts, n, stream=stream.cuda_stream)
-
-            def mult():
-                return ctx.mult(d_sc.data_ptr(), 32, on_device=True, stream=stream.cuda_stream)
-
-            def mult_batch(k):  # k MSMs on the same resident scalars, pipelined (set_stride 0)
-                return ctx.mult_batch(d_sc.data_ptr(), k, 32, set_stride=0, on_device=True,
-                                      stream=stream.cuda_stream)
-            ctx._bench_batch = mult_batch
+            ctx.build_table(pts, n, stream=sp)
         elif method == "bgmw":
             ctx = m.BGMWContext(G, local, n_exp=args.log_n)
-            ctx.build_table(pts, n, stream=stream.cuda_stream)
-
-            def mult():
-                return ctx.mult(d_sc.data_ptr(), 32, on_device=True, stream=stream.cuda_stream)
+            ctx.build_table(pts, n, stream=sp)
         else:
             ctx = m.MSMContext(G, local, args.window)
-            ctx.set_points(pts, n, stream=stream.cuda_stream)
-
-            def mult():
-                return ctx.mult(d_sc.data_ptr(), 255, stride=32, on_device=True, stream=stream.cuda_stream)
+            ctx.set_points(pts, n, stream=sp)
         torch.cuda.synchronize(dev)
         log(f"[rank {rank}] {method} setup {time.time() - t:.3f}s")
         ctx.set_profiling(True)
 
-        def step():
-            part = mult()
-            if world > 1:
-                return mdist.fold(mdist.gather_partials(part, G, dev), add)
-            return part
-        return ctx, step
+        def mult(k, on_device=True):
+            base = (dptr if on_device else hptr) + k * SS
+            if method == "pippenger":
+                return ctx.mult(base, 255, stride=32, on_device=on_device, stream=sp)
+            return ctx.mult(base, 32, on_device=on_device, stream=sp)
+        return ctx, mult
 
-    ctx, step = make(args.method)
+    def sync_steps(mult, k_steps, on_device):
+        """k_steps synchronous MSMs over sets 0..k_steps-1 (exchange + fold per step)."""
+        out = []
+        with Bracket(world, dev) as b:
+            for k in range(k_steps):
+                part = mult(k, on_device)
+                out.append(part if world == 1 else mdist.fold(mdist.gather_partials(part, G, dev), add))
+        return out, b.elapsed
+
+    ctx, mult = make(args.method)
     batched = args.method == "ches" and not args.no_batch
+    legs = {}
     if batched:
-        res, elapsed, acc_ms = timed_batch(ctx, args.steps, args.warmup, world, dev, add)
-        ctx.mult(d_sc.data_ptr(), 32, on_device=True, stream=stream.cuda_stream)  # one profiled single MSM
+        if W:
+            ctx.mult_batch(hptr, min(W, K), 32, set_stride=SS, on_device=False, stream=sp)
+        with Bracket(world, dev) as b:  # headline: host scalars, H2D inside the pipeline
+            parts = ctx.mult_batch(hptr, K, 32, set_stride=SS, on_device=False, stream=sp)
+            res = fold_all(parts)
+        elapsed, acc_ms = b.elapsed, ctx.phase_times()["accumulate"]
+        legs["ches_batch_h2d"] = {"value": round(n * world * K / elapsed, 1), "ms_per_step": round(elapsed / K * 1e3, 4),
+                                  "kernel_ms": round(acc_ms, 4),
+                                  "note": "headline: K distinct scalar sets in pinned host memory, H2D in the timed region"}
+        if not args.no_compare:
+            with Bracket(world, dev) as b:
+                rparts = fold_all(ctx.mult_batch(dptr, K, 32, set_stride=SS, on_device=True, stream=sp))
+            legs["ches_batch_resident"] = {"value": round(n * world * K / b.elapsed, 1),
+                                           "ms_per_step": round(b.elapsed / K * 1e3, 4),
+                                           "kernel_ms": round(ctx.phase_times()["accumulate"], 4),
+                                           "equals_h2d_batch": keys(rparts) == keys(res),
+                                           "note": "the same K sets already resident in HBM (kernel-only rate)"}
+            sres, sel = sync_steps(mult, K, True)
+            legs["ches_sync"] = {"value": round(n * world * K / sel, 1), "ms_per_step": round(sel / K * 1e3, 4),
+                                 "note": "K synchronous msm_ches_ctx_mult calls on resident sets (per-MSM latency)"}
+            batch_eq_sync = keys(sres) == keys(res)
+        else:
+            batch_eq_sync = None
+        mult(0)  # one profiled synchronous MSM for the phase split
         phases = ctx.phase_times()
     else:
-        res, elapsed, acc_ms, tot_ms, phases = timed_steps(step, ctx, args.steps, args.warmup, world, dev)
+        for k in range(W):
+            mult(k % K, False)
+        res, elapsed = sync_steps(mult, K, False)
+        phases = ctx.phase_times()
+        acc_ms = phases["accumulate"]
+        batch_eq_sync = None
+        legs[args.method + "_sync_h2d"] = {"value": round(n * world * K / elapsed, 1),
+                                           "ms_per_step": round(elapsed / K * 1e3, 4)}
 
+    # ---- parity ----
     gold = json.load(open(os.path.join(REPO, "tests", "golden", f"msm_g{G}.json")))
-    want = [c["compressed"] for c in gold["cases"] if c["n"] == n and c["seed"] == 1 and c["case"] == "rand"]
-    parity = (m.compress(G, res).hex() == want[0]) if (world == 1 and want) else None
+    want = [c["compressed"] for c in gold["cases"]
+            if c["n"] == n * world and c["seed"] == 1 and c["case"] == "rand"]
+    golden_ok = (m.compress(G, res[0]).hex() == want[0]) if want else None
+    cross = None
+    if world > 1 and not want:  # no golden for this total size: plain Pippenger on the same shard and set 0
+        pctx = m.MSMContext(G, local, args.window)
+        pctx.set_points(pts, n, stream=sp)
+        pp = pctx.mult(dptr, 255, stride=32, on_device=True, stream=sp)
+        mine = ctx.mult(dptr, 32, on_device=True, stream=sp) if args.method != "pippenger" else pp
+        cross = all_true(m.compress(G, pp) == m.compress(G, mine), world, dev)
+        pctx.close()
 
-    sync = None
-    if batched and world == 1 and not args.no_compare:  # the same MSMs issued one by one (no overlap)
-        sres, sel, _, _, sph = timed_steps(step, ctx, args.steps, 1, world, dev)
-        sync = {"value": round(n * args.steps / sel, 1), "unit": "pairs/s",
-                "ms_per_step": round(sel / args.steps * 1e3, 4),
-                "parity_vs_reference": (m.compress(G, sres).hex() == want[0]) if want else None,
-                "note": "K synchronous msm_ches_ctx_mult calls (per-MSM latency)"}
     others = {}
-    if world == 1 and not args.no_compare:  # the reference's other methods, same points and scalars
+    if world == 1 and not args.no_compare:  # the reference's other methods, same points, resident sets
         for ometh in ("ches", "pippenger", "bgmw"):
             if ometh == args.method:
                 continue
-            octx, ostep = make(ometh)
-            k = max(5, args.steps // 2)
-            ores, oel, oacc, _, oph = timed_steps(ostep, octx, k, 2, world, dev)
+            octx, omult = make(ometh)
+            k = max(5, K // 2)
+            for _ in range(2):
+                omult(0)
+            ores, oel = sync_steps(omult, k, True)
             others[ometh] = {"value": round(n * k / oel, 1), "unit": "pairs/s",
                              "ms_per_step": round(oel / k * 1e3, 4),
-                             "phases_ms": {kk: round(v, 4) for kk, v in oph.items()},
-                             "parity_vs_reference": (m.compress(G, ores).hex() == want[0]) if want else None}
+                             "phases_ms": {kk: round(v, 4) for kk, v in octx.phase_times().items()},
+                             "equals_headline": keys(ores) == keys(res[:k]),
+                             "parity_vs_reference": (m.compress(G, ores[0]).hex() == want[0]) if want else None}
             octx.close()
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(m, pts, host, n, K, res, G, args.cpu_sample_log_n if G == 1 else min(args.cpu_sample_log_n, 18))
 
     if rank != 0:
         if world > 1:
             torch.distributed.destroy_process_group()
         return
 
-    value = n * world * args.steps / elapsed
-    acc_s = sum(acc_ms) / len(acc_ms) / 1e3
+    value = n * world * K / elapsed
+    acc_s = acc_ms / 1e3
     if args.method == "ches":
         h = ctx.params["h"]
         madds = n * h                                 # one table point per (i, j) digit (SURVEY 8d)
         alg_bytes = n * h * AFFINE_BYTES * G              # h affine gathers per pair (SURVEY 8d: 1184 B/pair incl. scalar)
         workload = (f"G{G} MSM n=2^{args.log_n} per GPU, CHES nh+q/5 (q=2^{ctx.params['q_exp']}, h={h}, "
-                    f"|B|={ctx.params['b_size']}), table T=m*q^j*P_i resident in HBM, scalars resident in HBM")
+                    f"|B|={ctx.params['b_size']}), table T=m*q^j*P_i resident in HBM, K distinct scalar sets "
+                    f"H2D from pinned host memory inside the timed region")
         cfg_extra = {"method": "ches_q_over_5", "q_exp": ctx.params["q_exp"], "h": h,
                      "bucket_set": ctx.params["b_size"], "buckets_incl_top_digit_copies": ctx.bucket_count()}
     elif args.method == "bgmw":
@@ -241,14 +291,14 @@ def main():
         madds = n * h
         alg_bytes = n * h * AFFINE_BYTES * G
         workload = (f"G{G} MSM n=2^{args.log_n} per GPU, BGMW95 (q=2^{ctx.q_exp}, h={h}), table q^j*P_i resident in HBM, "
-                    f"scalars resident in HBM")
+                    f"scalars H2D per MSM")
         cfg_extra = {"method": "bgmw95", "q_exp": ctx.q_exp, "h": h}
     else:
-        W = (255 + 1 + args.window - 1) // args.window
-        madds = n * W
+        Wn = (255 + 1 + args.window - 1) // args.window
+        madds = n * Wn
         alg_bytes = n * (AFFINE_BYTES * G + 32)
-        workload = (f"G{G} MSM n=2^{args.log_n} per GPU, plain Pippenger c={args.window} ({W} windows), "
-                    f"points+scalars resident in HBM")
+        workload = (f"G{G} MSM n=2^{args.log_n} per GPU, plain Pippenger c={args.window} ({Wn} windows), "
+                    f"points resident in HBM, scalars H2D per MSM")
         cfg_extra = {"method": "pippenger", "window_bits": args.window}
     achieved_gbs = alg_bytes / acc_s / 1e9
     traffic = None
@@ -262,43 +312,43 @@ def main():
     fpm_per_madd = FPMUL_PER_MADD if G == 1 else 28   # Fp2: 8M + 2S = 8*3 + 2*2 Fp-mul
     fpmul_rate = madds * fpm_per_madd / acc_s
 
-    cpu = None
-    if world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(m, pts, sc, args.cpu_sample_log_n if G == 1 else min(args.cpu_sample_log_n, 18), G)
-
+    parity = golden_ok if golden_ok is not None else cross
+    if batch_eq_sync is False:
+        parity = False
     line = {
         "metric": METRIC if G == 1 else METRIC_G2,
         "value": round(value, 1),
         "unit": "pairs/s",
         "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "steps": K,
+        "warmup": W,
+        "ms_per_step": round(elapsed / K * 1e3, 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u32 (exact Fp381 integer arithmetic, 14x28-bit limbs)" + ("" if G == 1 else ", Fp2 = Fp[i]/(i^2+1)"),
-        "data": "synthetic: P_i = 2^(i+1) G1 (main_p1.cpp:52-66), SplitMix64 scalars < r (BASELINE.md sec.3)",
+        "data": ("synthetic: P_i = 2^(i+1) G%d (main_p1.cpp:52-66), SplitMix64 scalars < r (BASELINE.md sec.3), "
+                 "K distinct scalar sets" % G),
         "config": dict({"workload": workload, "n_per_gpu": n, "n_total": n * world,
                         "parallelism": f"points sharded x{world}, RCCL all_gather of {144 * G}-B partials"}, **cfg_extra),
         "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved_gbs / HBM_PEAK_GBS, 5), "traffic": traffic,
                      "kernel": "k_accumulate (bucket accumulation)", "kernel_ms": round(acc_s * 1e3, 4),
+                     "kernel_ms_basis": "HIP events around each accumulation of the timed batch, on its stream",
                      "algorithmic_bytes_per_launch": alg_bytes,
                      "note": "integer-VALU bound (v_mad_u64_u32 issue), see valu_roofline"},
         "valu_roofline": {"bound": "valu-int", "achieved": round(fpmul_rate / 1e9, 2),
                           "peak": round(FPMUL_PEAK / 1e9, 2), "unit": "G Fp-mul/s",
                           "frac": round(fpmul_rate / FPMUL_PEAK, 4),
                           "work": f"{madds} xyzz madds x {fpm_per_madd} Fp-mul",
-                          "peak_basis": "measured register-resident Fp-mul kernel (tools/microbench/fp_rate.hip)"},
+                          "peak_basis": "measured register-resident Fp-mul kernel (profiles/r02_fp_rate.txt)"},
         "phases_ms": {k: round(v, 4) for k, v in phases.items()},
         "phases_note": "one synchronous MSM (profiled) after the timed region" if batched else "last timed step",
         "pipelined_batch": batched,
         "parity_vs_reference": parity,
-        "methods": {args.method + ("_batch" if batched else ""): {"value": round(value, 1),
-                                                                   "ms_per_step": round(elapsed / args.steps * 1e3, 4)},
-                    **({"ches_sync": sync} if sync else {}),
-                    **others},
+        "parity_detail": {"set0_vs_golden": golden_ok, "batch_equals_sync_all_sets": batch_eq_sync,
+                          "pippenger_cross_check_all_ranks": cross},
+        "methods": dict(legs, **others),
         "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)
@@ -306,50 +356,72 @@ def main():
         torch.distributed.destroy_process_group()
 
 
-def cpu_baseline(m, pts, sc, log_n, G=1):
-    """The reference's own blst_p{1,2}s_mult_pippenger (libblst built from /root/reference
-    sources into oracle/_ref/libblst_ref.so, x86-64 mulx asm), 1 thread -- the
-    reference has no threading -- timed on this host's cores on the same points and
-    scalars; falls back to the oracle port (oracle/msm_oracle.c) if the reference
-    build is absent.  The result is cross-checked against the GPU result."""
-    import ctypes
-    k = 1 << log_n
+def _ref_lib(name):
+    p = os.path.join(REPO, "oracle", "_ref", name)
+    return ctypes.CDLL(p) if os.path.exists(p) else None
+
+
+def cpu_baseline(m, pts, host, n, K, gpu_res, G, log_n):
+    """The reference's own blst_p{G}s_mult_pippenger (libblst built from the
+    /root/reference sources into oracle/_ref, x86-64 mulx asm) on the host cores:
+    1 thread (the reference driver is single-threaded) on set 0, and all of this
+    GPU's CPU share (CPU_THREADS) through the Go binding's tile grid
+    (oracle/ref_grid.c over the reference's blst_p{G}s_tile_pippenger) on the last
+    set; both cross-checked against the GPU.  Falls back to the oracle port when
+    the reference build is absent."""
+    k = min(1 << log_n, n)
+    sc = host.numpy()
     P = (ctypes.c_uint8 * (96 * G * k)).from_buffer_copy(bytes(pts)[:96 * G * k])
-    S = (ctypes.c_uint8 * (32 * k)).from_buffer_copy(bytes(sc)[:32 * k])
-    ref_so = os.path.join(REPO, "oracle", "_ref", "libblst_ref.so")
-    if os.path.exists(ref_so):
-        R = ctypes.CDLL(ref_so)
+    S0 = (ctypes.c_uint8 * (32 * k)).from_buffer_copy(sc[:32 * k].tobytes())
+    last = (K - 1) * n * 32
+    SL = (ctypes.c_uint8 * (32 * k)).from_buffer_copy(sc[last:last + 32 * k].tobytes())
+    full = k == n
+    R = _ref_lib("libblst_ref.so")
+    out = {}
+    if R is not None:
         sizeof = getattr(R, f"blst_p{G}s_mult_pippenger_scratch_sizeof")
         sizeof.restype = ctypes.c_size_t
         sizeof.argtypes = [ctypes.c_size_t]
         mult = getattr(R, f"blst_p{G}s_mult_pippenger")
-        mult.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
-                         ctypes.c_void_p]
+        mult.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
         scratch = (ctypes.c_uint8 * sizeof(k))()
         pp = (ctypes.c_void_p * 2)(ctypes.cast(P, ctypes.c_void_p), None)
-        sp = (ctypes.c_void_p * 2)(ctypes.cast(S, ctypes.c_void_p), None)
+        sp = (ctypes.c_void_p * 2)(ctypes.cast(S0, ctypes.c_void_p), None)
         r = (ctypes.c_uint8 * (144 * G))()
         t = time.perf_counter()
         mult(r, pp, k, sp, 255, scratch)
-        dt = time.perf_counter() - t
-        out = (ctypes.c_uint8 * (48 * G))()
-        getattr(R, f"blst_p{G}_compress")(out, r)
-        cpu_res, kind = bytes(out).hex(), "reference"
-        what = f"reference libblst blst_p{G}s_mult_pippenger (oracle/_ref)"
+        dt1 = time.perf_counter() - t
+        one = {"value": round(k / dt1, 1), "cores": 1, "seconds": round(dt1, 2),
+               "matches_gpu": (m.compress(G, bytes(r)) == m.compress(G, gpu_res[0])) if full else None}
+        kind = "reference"
+        Gd = _ref_lib("libref_grid.so")
+        if Gd is not None:
+            Gd.ref_grid_msm.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                        ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+            r2 = (ctypes.c_uint8 * (144 * G))()
+            t = time.perf_counter()
+            Gd.ref_grid_msm(G, r2, P, k, SL, 255, CPU_THREADS)
+            dtn = time.perf_counter() - t
+            multi = {"value": round(k / dtn, 1), "cores": CPU_THREADS, "seconds": round(dtn, 2),
+                     "matches_gpu": (m.compress(G, bytes(r2)) == m.compress(G, gpu_res[-1])) if full else None,
+                     "what": f"Go-binding tile grid (bindings/go/blst.go:2064-2197) over the reference's "
+                             f"blst_p{G}s_tile_pippenger, {CPU_THREADS} threads, last scalar set"}
+        else:
+            multi = None
+        out = {"value": one["value"], "unit": "pairs/s", "cores": 1, "kind": kind,
+               "sample": f"reference libblst blst_p{G}s_mult_pippenger (oracle/_ref), 1 thread, "
+                         f"first 2^{log_n} points, scalar set 0, {dt1:.1f}s",
+               "matches_gpu": one["matches_gpu"], "all_cores": multi}
     else:
         sys.path.insert(0, os.path.join(REPO, "tests"))
         import oracle_ffi as of
         t = time.perf_counter()
-        r = of.msm(G, P, S, k, 255, "pippenger")
-        dt = time.perf_counter() - t
-        cpu_res, kind, what = of.compress(G, r), "port", "oracle port of blst Pippenger (oracle/msm_oracle.c)"
-    ctx = m.CHESContext(G, 0, n_exp=log_n)
-    ctx.build_table(P, k)
-    gpu_res = m.compress(G, ctx.mult(S)).hex()
-    ctx.close()
-    return {"value": round(k / dt, 1), "unit": "pairs/s", "cores": 1, "kind": kind,
-            "sample": f"{what}, 1 thread, first 2^{log_n} points/scalars of the rank-0 workload, {dt:.1f}s",
-            "matches_gpu": cpu_res == gpu_res}
+        r = of.msm(G, P, S0, k, 255, "pippenger")
+        dt1 = time.perf_counter() - t
+        out = {"value": round(k / dt1, 1), "unit": "pairs/s", "cores": 1, "kind": "port",
+               "sample": f"oracle port of blst Pippenger (oracle/msm_oracle.c), 1 thread, 2^{log_n} pairs, {dt1:.1f}s",
+               "matches_gpu": (of.compress(G, r) == m.compress(G, gpu_res[0]).hex()) if full else None}
+    return out
 
 
 if __name__ == "__main__":

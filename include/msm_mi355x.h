@@ -204,7 +204,10 @@ int msm_ches_ctx_mult(msm_ches_ctx *ctx, void *ret, const byte *scalars, size_t 
  * MSM k's latency-bound bucket-reduction tail runs on a second stream beside
  * MSM k+1's digit conversion, sort and accumulation (the batched-MSM shape of a
  * prover committing many polynomials to one SRS).  Results equal count calls
- * of msm_ches_ctx_mult. */
+ * of msm_ches_ctx_mult.  Host scalars (scalars_on_device = 0) are copied set by
+ * set inside the pipeline, each copy overlapping earlier MSMs' accumulations;
+ * pass page-locked memory (hipHostMalloc / hipHostRegister) for the copies to
+ * be asynchronous. */
 int msm_ches_ctx_mult_batch(msm_ches_ctx *ctx, void *rets, const byte *scalars, size_t stride, size_t set_stride,
                             size_t count, int scalars_on_device, void *hip_stream);
 /* table file cache (the reference rebuilds its tables on every run, main_p1.cpp:128-178):

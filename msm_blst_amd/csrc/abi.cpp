@@ -738,21 +738,15 @@ int msm_ches_ctx_mult_batch(msm_ches_ctx *ctx, void *rets, const byte *scalars, 
   try {
     DeviceGuard g(ctx->device);
     hipStream_t s = (hipStream_t)stream;
-    size_t n = CHES_DISPATCH(ctx, npoints());
-    const uint8_t *d = scalars;
-    if (!on_device && n && count) {
-      size_t span = (count - 1) * set_stride + n * stride;
-      ctx->scalars.ensure(span + 16);
-      MSM_HIP_CHECK(hipMemcpyAsync(ctx->scalars.p, scalars, span, hipMemcpyHostToDevice, s));
-      d = ctx->scalars.as<uint8_t>();
-    }
+    // host scalars are streamed set by set inside the pipeline (Ches::run_batch)
+    const bool on_host = !on_device;
     if (ctx->group == 1) {
       std::vector<hfp::Jac<hfp::Fp>> out(count);
-      ctx->g1->run_batch(s, d, stride, set_stride, count, out.data());
+      ctx->g1->run_batch(s, scalars, stride, set_stride, count, out.data(), on_host);
       memcpy(rets, out.data(), count * sizeof(out[0]));
     } else {
       std::vector<hfp::Jac<hfp::Fp2>> out(count);
-      ctx->g2->run_batch(s, d, stride, set_stride, count, out.data());
+      ctx->g2->run_batch(s, scalars, stride, set_stride, count, out.data(), on_host);
       memcpy(rets, out.data(), count * sizeof(out[0]));
     }
     return MSM_OK;
@@ -1046,3 +1040,4 @@ int msm_test_xyzz(int group, const void *pts, size_t npts, const uint32_t *ops, 
 }
 
 }  // extern "C"
+

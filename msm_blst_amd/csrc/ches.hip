@@ -246,18 +246,29 @@ void WeightedReducer<G>::plan(const std::vector<uint32_t> &w, const std::vector<
   idx_.ensure(std::max<size_t>(all.size(), 1) * 4);
   if (!all.empty()) MSM_HIP_CHECK(hipMemcpy(idx_.p, all.data(), all.size() * 4, hipMemcpyHostToDevice));
   final_perm_off_ = idx.size();
-  size_t maxp = 1;
-  for (size_t l = 0; l + 1 < nout_.size(); ++l) maxp = std::max(maxp, nout_[l]);
-  for (int st = 0; st < NSETS; ++st) {
-    part_[st][0].ensure(maxp * sizeof(Xyzz<F>));
-    part_[st][1].ensure(maxp * sizeof(Xyzz<F>));
-    dense_buf_[st].ensure(NS * sizeof(Xyzz<F>));
+  maxp_ = 1;
+  for (size_t l = 0; l + 1 < nout_.size(); ++l) maxp_ = std::max(maxp_, nout_[l]);
+  for (int st = 0; st < NSETS; ++st) {  // a new plan: sets are (re)sized on their next use
+    part_[st][0].release();
+    part_[st][1].release();
+    dense_buf_[st].release();
   }
+  ensure_set(0);
+}
+
+template <int G>
+void WeightedReducer<G>::ensure_set(int set) {
+  typedef typename FieldOf<G>::F F;
+  if (set < 0 || set >= NSETS) throw std::runtime_error("WeightedReducer: bad buffer set");
+  part_[set][0].ensure(maxp_ * sizeof(Xyzz<F>));
+  part_[set][1].ensure(maxp_ * sizeof(Xyzz<F>));
+  dense_buf_[set].ensure((size_t)2 * nwin_ * ((size_t)1 << sbits_) * sizeof(Xyzz<F>));
 }
 
 template <int G>
 void WeightedReducer<G>::launch_head(hipStream_t s, const void *Sbuf, int set) {
   typedef typename FieldOf<G>::F F;
+  ensure_set(set);
   const size_t L = nout_.size();
   const Xyzz<F> *src = reinterpret_cast<const Xyzz<F> *>(Sbuf);
   Xyzz<F> *dst = L == 1 ? dense_buf_[set].as<Xyzz<F>>() : part_[set][0].as<Xyzz<F>>();
@@ -340,18 +351,13 @@ Ches<G>::~Ches() {
   for (auto &e : ev_) (void)hipEventDestroy(e);
   for (auto &e : acc_ev_) (void)hipEventDestroy(e);
   for (auto &e : bev_) (void)hipEventDestroy(e);
-  for (int k = 0; k < 2; ++k) {
-    if (ev_head_[k]) (void)hipEventDestroy(ev_head_[k]);
-    if (ev_tail_[k]) (void)hipEventDestroy(ev_tail_[k]);
-    if (host_out_[k]) (void)hipHostFree(host_out_[k]);
+  for (int t = 0; t < kBSets; ++t) {
+    if (ev_tail_[t]) (void)hipEventDestroy(ev_tail_[t]);
+    if (tails_[t]) (void)hipStreamDestroy(tails_[t]);
   }
-  for (int k = 0; k < 2; ++k) {
-    if (ev_front_[k]) (void)hipEventDestroy(ev_front_[k]);
-    if (ev_acc_[k]) (void)hipEventDestroy(ev_acc_[k]);
-  }
-  for (int k = 0; k < 2; ++k)
-    if (tails_[k]) (void)hipStreamDestroy(tails_[k]);
+  if (host_out_) (void)hipHostFree(host_out_);
   if (fstream_) (void)hipStreamDestroy(fstream_);
+  if (cstream_) (void)hipStreamDestroy(cstream_);
 }
 
 // bucket space = B plus (copies_ - 1) copies of the small buckets 1..small_;
@@ -540,8 +546,8 @@ void Ches<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, hfp::J
 }
 
 template <int G>
-void Ches<G>::run_batch(hipStream_t s, const uint8_t *d_scalars, size_t stride, size_t set_stride, size_t count,
-                        hfp::Jac<HF> *outs) {
+void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, size_t set_stride, size_t count,
+                        hfp::Jac<HF> *outs, bool scalars_on_host) {
   DeviceGuard g(dev_);
   if (stride < 32) throw std::runtime_error("CHES scalars must be 32-byte strings");
   if (count == 0) return;
@@ -550,31 +556,38 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *d_scalars, size_t stride, 
     return;
   }
   if (!fstream_) {
-    // the short digit/sort and latency-bound reduction kernels go ahead of the
-    // long accumulation's pending workgroups: highest stream priority
-    // (measured alternatives -- tails at the lowest priority, accumulations on
-    // their own stream, front k+1 before head k -- were slower or equal)
+    // fronts at the greatest priority: their short memory-bound kernels take the
+    // first CU slots an accumulation releases (the next accumulation waits for
+    // them); the reductions at normal priority, beside the accumulations (the
+    // same priority for both measured equal, tools/batch_sched.py)
     int least = 0, greatest = 0;
     MSM_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    for (int k = 0; k < 2; ++k)
-      MSM_HIP_CHECK(hipStreamCreateWithPriority(&tails_[k], hipStreamNonBlocking, greatest));
     MSM_HIP_CHECK(hipStreamCreateWithPriority(&fstream_, hipStreamNonBlocking, greatest));
-    for (int k = 0; k < 2; ++k) {
-      MSM_HIP_CHECK(hipEventCreateWithFlags(&ev_head_[k], hipEventDisableTiming));
-      MSM_HIP_CHECK(hipEventCreateWithFlags(&ev_tail_[k], hipEventDisableTiming));
-      MSM_HIP_CHECK(hipEventCreateWithFlags(&ev_front_[k], hipEventDisableTiming));
-      MSM_HIP_CHECK(hipEventCreateWithFlags(&ev_acc_[k], hipEventDisableTiming));
+    for (int t = 0; t < kBSets; ++t) {
+      MSM_HIP_CHECK(hipStreamCreateWithPriority(&tails_[t], hipStreamNonBlocking, 0));
+      MSM_HIP_CHECK(hipEventCreateWithFlags(&ev_tail_[t], hipEventDisableTiming));
     }
+    MSM_HIP_CHECK(hipStreamCreateWithFlags(&cstream_, hipStreamNonBlocking));
   }
   // one pinned read-back slot per MSM of the batch: the host never waits inside
   // the issue loop, so MSM k+1's front is queued while MSM k still accumulates
   const size_t ob = (red_.out_bytes() + 255) & ~(size_t)255;
   if (host_out_bytes_ < count * ob) {
-    if (host_out_[0]) (void)hipHostFree(host_out_[0]);
-    host_out_[0] = nullptr;
-    MSM_HIP_CHECK(hipHostMalloc(&host_out_[0], count * ob, hipHostMallocDefault));
+    if (host_out_) (void)hipHostFree(host_out_);
+    host_out_ = nullptr;
+    host_out_bytes_ = 0;
+    MSM_HIP_CHECK(hipHostMalloc(&host_out_, count * ob, hipHostMallocDefault));
     host_out_bytes_ = count * ob;
   }
+  // every buffer the loop touches exists before the first launch (an allocation
+  // inside the issue loop could synchronise the device)
+  const size_t NB = bucket_count(), n = n_;
+  for (int b = 0; b < kBSets && (size_t)b < count; ++b) {
+    buckets_[b].ensure(NB * sizeof(Xyzz<typename FieldOf<G>::F>));
+    red_.ensure_set(b);
+  }
+  if (scalars_on_host)
+    for (int f = 0; f < kSlots && (size_t)f < count; ++f) scal_[f].ensure(n * stride + 16);
   const bool prof = profile_;
   profile_ = false;
   if (prof)
@@ -583,54 +596,76 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *d_scalars, size_t stride, 
       MSM_HIP_CHECK(hipEventCreate(&e));
       acc_ev_.push_back(e);
     }
-  // Four streams, three front sets (k % 3) and two bucket sets (k & 1):
-  //   fstream_:  digits + sort of MSM k into front set k%3 (after MSM k-3's
-  //              accumulation released it).  The accumulation fills every CU
-  //              slot until its last workgroups are dispatched, so a front only
-  //              gets the chip in an accumulation's tail: with three sets, MSM
-  //              k+1's front runs in MSM k-1's tail, not in MSM k's, and is
-  //              ready before MSM k's accumulation ends;
-  //   s:         accumulation k into bucket set k&1 (after MSM k-2's reduction
-  //              head released it) -- back to back, the VALU-bound critical path;
-  //   tails_[set]: the whole reduction of MSM k (level 0, latency-bound tail,
-  //              read-back) beside the next accumulations.
+  // Streams, kFronts front sets (k % kFronts), kBSets bucket sets (k % kBSets)
+  // and, for host scalars, kSlots device scalar slots (k % kSlots):
+  //   fstream_:  digits + sort of MSM k into front set k % kFronts (after MSM
+  //              k - kFronts's accumulation released it).  The accumulation fills
+  //              every CU slot until its last workgroups are dispatched, so a front
+  //              only gets the chip in an accumulation's tail: with three sets, MSM
+  //              k+1's front runs in MSM k-1's tail and is ready before MSM k's
+  //              accumulation ends;
+  //   s:         accumulation k into bucket set k % kBSets (after MSM k-2's
+  //              reduction head released it) -- back to back, the VALU-bound
+  //              critical path;
+  //   tails_[t]: the whole reduction of MSM k, t = k % kBSets (level 0,
+  //              latency-bound tail, read-back) beside the next accumulations --
+  //              two streams, so MSM k+1's level 0 never queues behind MSM k's
+  //              latency-bound tail (one shared stream: 352 vs 412 M pairs/s);
+  //   cstream_:  host scalars: the H2D copy of set k + kSlots into the slot front
+  //              k has consumed, on its own stream (copies on the front stream:
+  //              -5 %, on the reduction streams: -15 %; own stream: -2 % vs
+  //              resident scalars).
   // No host waits inside the loop: every MSM has its own pinned read-back slot.
-  // per-MSM events (never re-recorded inside one batch)
-  while (bev_.size() < 3 * count + 1) {
+  while (bev_.size() < 4 * count + 1) {
     hipEvent_t e;
     MSM_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     bev_.push_back(e);
   }
-  hipEvent_t *evf = bev_.data() + 1, *eva = evf + count, *evh = eva + count;  // front, acc, head of MSM k
+  hipEvent_t *evf = bev_.data() + 1, *eva = evf + count, *evh = eva + count, *evc = evh + count;
   MSM_HIP_CHECK(hipEventRecord(bev_[0], s));  // the batch starts after prior work on s
   MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, bev_[0], 0));
-  auto issue_front = [&](size_t k) {
-    if (k >= (size_t)kFronts) MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, eva[k - kFronts], 0));  // front set free
-    digits_sort(fstream_, d_scalars + k * set_stride, stride, (int)(k % kFronts));
-    MSM_HIP_CHECK(hipEventRecord(evf[k], fstream_));
+  for (int t = 0; t < kBSets; ++t) MSM_HIP_CHECK(hipStreamWaitEvent(tails_[t], bev_[0], 0));
+  auto copy_set = [&](size_t k) {
+    if (!scalars_on_host || k >= count) return;
+    MSM_HIP_CHECK(hipMemcpyAsync(scal_[k % kSlots].p, scalars + k * set_stride, n * stride, hipMemcpyHostToDevice,
+                                 cstream_));
+    MSM_HIP_CHECK(hipEventRecord(evc[k], cstream_));
   };
-  hipStream_t as = s;
+  for (size_t k = 0; k < (size_t)kSlots; ++k) copy_set(k);
   for (size_t k = 0; k < count; ++k) {
-    issue_front(k);
-    const int set = (int)(k & 1), fset = (int)(k % kFronts);
-    MSM_HIP_CHECK(hipStreamWaitEvent(as, evf[k], 0));
-    if (k >= 2) MSM_HIP_CHECK(hipStreamWaitEvent(as, evh[k - 2], 0));  // bucket set free again
-    if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k], as));
-    accumulate(as, fset, set);
-    if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k + 1], as));
-    MSM_HIP_CHECK(hipEventRecord(eva[k], as));
-    MSM_HIP_CHECK(hipStreamWaitEvent(tails_[set], eva[k], 0));
-    red_.launch_head(tails_[set], buckets_[set].p, set);
-    MSM_HIP_CHECK(hipEventRecord(evh[k], tails_[set]));
-    red_.launch_tail(tails_[set], set, false);  // beside the accumulations: least resource time
-    red_.copy_out(tails_[set], set, (uint8_t *)host_out_[0] + k * ob);
+    const int bset = (int)(k % kBSets), fset = (int)(k % kFronts);
+    hipStream_t ts = tails_[bset];
+    const uint8_t *src = scalars + k * set_stride;
+    if (scalars_on_host) {
+      src = scal_[k % kSlots].as<uint8_t>();
+      MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, evc[k], 0));
+    }
+    if (k >= (size_t)kFronts) MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, eva[k - kFronts], 0));  // front set free
+    digits_sort(fstream_, src, stride, fset);
+    MSM_HIP_CHECK(hipEventRecord(evf[k], fstream_));
+    if (scalars_on_host && k + kSlots < count) {  // set k + kSlots into the slot front k has consumed
+      MSM_HIP_CHECK(hipStreamWaitEvent(cstream_, evf[k], 0));
+      copy_set(k + kSlots);
+    }
+    MSM_HIP_CHECK(hipStreamWaitEvent(s, evf[k], 0));
+    if (k >= (size_t)kBSets) MSM_HIP_CHECK(hipStreamWaitEvent(s, evh[k - kBSets], 0));  // bucket set free again
+    if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k], s));
+    accumulate(s, fset, bset);
+    if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k + 1], s));
+    MSM_HIP_CHECK(hipEventRecord(eva[k], s));
+    MSM_HIP_CHECK(hipStreamWaitEvent(ts, eva[k], 0));
+    red_.launch_head(ts, buckets_[bset].p, bset);
+    MSM_HIP_CHECK(hipEventRecord(evh[k], ts));
+    red_.launch_tail(ts, bset, false);  // beside the accumulations: least resource time
+    red_.copy_out(ts, bset, (uint8_t *)host_out_ + k * ob);
   }
-  for (int t = 0; t < 2; ++t) {  // the caller's stream observes completion of every reduction
+  // the caller's stream observes completion of every reduction (and front)
+  for (int t = 0; t < kBSets; ++t) {
     MSM_HIP_CHECK(hipEventRecord(ev_tail_[t], tails_[t]));
     MSM_HIP_CHECK(hipStreamWaitEvent(s, ev_tail_[t], 0));
   }
-  for (int t = 0; t < 2; ++t) MSM_HIP_CHECK(hipStreamSynchronize(tails_[t]));
-  for (size_t k = 0; k < count; ++k) outs[k] = red_.combine((const uint8_t *)host_out_[0] + k * ob)[0];
+  for (int t = 0; t < kBSets; ++t) MSM_HIP_CHECK(hipStreamSynchronize(tails_[t]));
+  for (size_t k = 0; k < count; ++k) outs[k] = red_.combine((const uint8_t *)host_out_ + k * ob)[0];
   profile_ = prof;
   if (prof) {  // average accumulation time over the batch (HIP events on stream s)
     float sum = 0;

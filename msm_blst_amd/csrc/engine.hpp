@@ -143,7 +143,7 @@ template <int G>
 class WeightedReducer {
  public:
   typedef typename HostField<G>::F HF;
-  static constexpr int NSETS = 2;
+  static constexpr int NSETS = 2;  // buffer sets, allocated on first use (Ches batch: one per bucket set)
   // win[i] in [0, nwin): the window of bucket i (empty = all in window 0)
   void plan(const std::vector<uint32_t> &w, const std::vector<uint32_t> &win, int nwin);
   void plan(const std::vector<uint32_t> &w) { plan(w, {}, 1); }
@@ -161,8 +161,10 @@ class WeightedReducer {
   hfp::Jac<HF> read(hipStream_t s) { return read_windows(s)[0]; }
   size_t size() const { return bsize_; }
 
+  void ensure_set(int set);  // allocate buffer set `set` for the current plan
+
  private:
-  size_t bsize_ = 0, final_perm_off_ = 0;
+  size_t bsize_ = 0, final_perm_off_ = 0, maxp_ = 1;
   int sbits_ = 1, nwin_ = 1;
   DevBuf idx_, dense_buf_[NSETS], part_[NSETS][2];
   std::vector<DevBuf> starts_;
@@ -224,10 +226,14 @@ class Ches {
   size_t table_rows() const { return 3 * (size_t)p_.h * n_; }
   // scalars: n 32-byte LE strings (stride >= 32) on device
   void run(hipStream_t s, const uint8_t *d_scalars, size_t stride, hfp::Jac<HF> *out);
-  // `count` MSMs over the same points; scalar set k at d_scalars + k * set_stride.
-  // Pipelined: MSM k's reduction tail runs on a second stream, beside MSM k+1.
-  void run_batch(hipStream_t s, const uint8_t *d_scalars, size_t stride, size_t set_stride, size_t count,
-                 hfp::Jac<HF> *outs);
+  // `count` MSMs over the same points; scalar set k at scalars + k * set_stride,
+  // in device memory or (scalars_on_host) host memory -- then each set is copied
+  // into one of kFronts device slots right before its digit conversion, on the
+  // front stream, overlapping earlier MSMs' accumulations (pinned host memory
+  // for a truly asynchronous copy).  Pipelined: MSM k's reduction runs on a
+  // second stream beside MSM k+1's accumulation.
+  void run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, size_t set_stride, size_t count,
+                 hfp::Jac<HF> *outs, bool scalars_on_host = false);
   size_t npoints() const { return n_; }
   const ChesParams &params() const { return p_; }
   size_t bucket_count() const { return B_.size() + (size_t)(copies_ - 1) * small_; }
@@ -247,17 +253,21 @@ class Ches {
   void plan_buckets(size_t n);
   bool profile_ = false;
   PhaseTimes times_;
-  DevBuf code_, rank_, table_, buckets_[2];  // buckets double-buffered: MSM k's reduction reads set k&1
-  // digit/sort outputs, double-buffered so that MSM k+1's digits and sort
-  // (memory/LDS-bound) run beside MSM k's accumulation (VALU-bound) in a batch
+  // bucket sets: MSM k accumulates into set k % kBSets while the reduction of
+  // MSM k-1 still reads the other one
+  static constexpr int kBSets = 2;
+  DevBuf code_, rank_, table_, buckets_[kBSets];
+  // digit/sort outputs, one set per in-flight front so that MSM k+1's digits
+  // and sort (memory/LDS-bound) run beside MSM k's accumulation (VALU-bound)
   static constexpr int kFronts = 3;  // batch: front k+1 runs in MSM k-1's accumulation tail
   ChesFrontSet fs_[kFronts];
+  static constexpr int kSlots = 4;   // device slots of host scalar sets in a batch
+  DevBuf scal_[kSlots];
   WeightedReducer<G> red_;
   std::vector<hipEvent_t> ev_;
-  hipStream_t tails_[2] = {nullptr, nullptr}, fstream_ = nullptr;
-  hipEvent_t ev_head_[2] = {nullptr, nullptr}, ev_tail_[2] = {nullptr, nullptr};
-  hipEvent_t ev_front_[2] = {nullptr, nullptr}, ev_acc_[2] = {nullptr, nullptr};
-  void *host_out_[2] = {nullptr, nullptr};
+  hipStream_t tails_[kBSets] = {nullptr, nullptr}, fstream_ = nullptr, cstream_ = nullptr;  // batch streams (+ the caller's)
+  hipEvent_t ev_tail_[kBSets] = {nullptr, nullptr};
+  void *host_out_ = nullptr;
   size_t host_out_bytes_ = 0;
   std::vector<hipEvent_t> bev_;     // batch dependency events, one per (MSM, stage)
   std::vector<hipEvent_t> acc_ev_;  // batch profiling: events around each accumulation

@@ -37,6 +37,21 @@ def gather_partials(partial: bytes, group: int, device=None):
     return [bytes(o.cpu().numpy().tobytes()) for o in outs]
 
 
+def gather_partials_batch(partials, group: int, device=None):
+    """One all_gather for a whole batch: partials[k] is this rank's Jacobian of
+    MSM k; returns, per MSM k, the list of every rank's partial (rank order)."""
+    nb = JAC_BYTES[group]
+    assert all(len(p) == nb for p in partials)
+    world = dist.get_world_size()
+    t = torch.frombuffer(bytearray(b"".join(partials)), dtype=torch.uint8)
+    if device is not None:
+        t = t.to(device)
+    outs = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(outs, t)
+    raw = [bytes(o.cpu().numpy().tobytes()) for o in outs]
+    return [[r[k * nb:(k + 1) * nb] for r in raw] for k in range(len(partials))]
+
+
 def fold(partials, add_fn):
     """Sum a list of Jacobian byte strings with an exact EC add (host, rank order)."""
     acc = partials[0]

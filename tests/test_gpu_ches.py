@@ -142,3 +142,26 @@ def test_mult_batch_matches_single(m, golden):
     rep = ctx.mult_batch(sets[0], 3, set_stride=0)  # one set repeated
     assert all(m.compress(1, r).hex() == _golden(golden, 1, n) for r in rep)
     ctx.close()
+
+
+@pytest.mark.parametrize("group,log_n", [(1, 16), (2, 10)])
+def test_mult_batch_sets_resident_and_pinned(m, group, log_n):
+    """Batches longer than every ring (3 front sets, 3 bucket sets, 3 scalar
+    slots): 7 distinct sets from device memory and from page-locked host memory
+    (streamed set by set inside the pipeline) equal the synchronous MSMs."""
+    import numpy as np
+    import torch
+    n, K = 1 << log_n, 7
+    ctx = m.CHESContext(group, 0, n_exp=log_n)
+    ctx.build_table(m.fixed_points(group, n), n)
+    host = torch.empty(K * n * 32, dtype=torch.uint8, pin_memory=True)
+    for k in range(K):
+        host.numpy()[k * n * 32:(k + 1) * n * 32] = np.frombuffer(m.gen_scalars(n, 100 + k), dtype=np.uint8)
+    dev = host.to("cuda:0")
+    torch.cuda.synchronize()
+    want = [m.compress(group, ctx.mult(dev.data_ptr() + k * n * 32, on_device=True)) for k in range(K)]
+    got_d = ctx.mult_batch(dev.data_ptr(), K, set_stride=n * 32, on_device=True)
+    got_h = ctx.mult_batch(host.data_ptr(), K, set_stride=n * 32, on_device=False)
+    assert [m.compress(group, r) for r in got_d] == want
+    assert [m.compress(group, r) for r in got_h] == want
+    ctx.close()

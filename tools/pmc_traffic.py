@@ -1,28 +1,51 @@
-"""Convert a rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE collection into the bench's
+"""Convert rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes into the bench's
 `roofline.traffic` figure: HBM bytes per k_accumulate launch.
 
-FETCH_SIZE/WRITE_SIZE are in KiB.  MI355X_MICROARCH.md (HBM section): on gfx950
-FETCH_SIZE reports half the bytes of wide (16 B/lane) reads -> x2; WRITE_SIZE
-is exact for 16 B/lane stores.  Our gathers are 16 B/lane loads of 112-B rows.
-usage: python tools/pmc_traffic.py <counter_collection.csv[,second_pass.csv]> <method> <log_n> [out.json]
+FETCH_SIZE/WRITE_SIZE are in KiB.  Calibration (tools/microbench/gather_cal.hip,
+profiles/r02_gather_cal.json): for a coalesced 16-B/lane stream FETCH_SIZE is half
+the bytes (MI355X_MICROARCH.md, HBM section); for the accumulation's pattern --
+each lane gathering one random 128-B table row with seven 16-B loads -- FETCH_SIZE
+is 64 B per row, i.e. x2 gives the full 128-B lines.  So FETCH x2 counts whole
+128-B lines; WRITE_SIZE is exact for 16-B/lane stores.
+usage: python tools/pmc_traffic.py <fetch.csv> <write.csv> <method> <log_n> [out.json] [calibration.json]
 """
 import csv
 import json
 import sys
 
-rows = [r for f in sys.argv[1].split(",") for r in csv.DictReader(open(f))]
-vals = {}
-for r in rows:
-    if "k_accumulate" not in r["Kernel_Name"]:
-        continue
-    vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
-fetch = sum(vals.get("FETCH_SIZE", [0])) / max(1, len(vals.get("FETCH_SIZE", [])))
-write = sum(vals.get("WRITE_SIZE", [0])) / max(1, len(vals.get("WRITE_SIZE", [])))
-out = {"method": sys.argv[2], "log_n": int(sys.argv[3]), "kernel": "k_accumulate",
-       "fetch_size_kib_raw": fetch, "write_size_kib_raw": write, "launches": len(vals.get("FETCH_SIZE", [])),
-       "accumulate_bytes_per_launch": int(fetch * 1024 * 2 + write * 1024),
-       "correction": "FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM section), WRITE_SIZE x1"}
+
+def per_kernel(path, counter):
+    vals = {}
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        name = r["Kernel_Name"].split("(")[0].replace("void ", "")
+        vals.setdefault(name, []).append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in vals.items()}
+
+
+fetch = per_kernel(sys.argv[1], "FETCH_SIZE")
+write = per_kernel(sys.argv[2], "WRITE_SIZE")
+acc = [k for k in fetch if "k_accumulate" in k][0]
+f_kib, w_kib = fetch[acc], write.get(acc, 0.0)
+out = {"method": sys.argv[3], "log_n": int(sys.argv[4]), "group": 1, "kernel": "k_accumulate",
+       "fetch_size_kib_raw": f_kib, "write_size_kib_raw": w_kib,
+       "accumulate_bytes_per_launch": int(f_kib * 1024 * 2 + w_kib * 1024),
+       "correction": "FETCH_SIZE x2 (whole 128-B lines, calibrated by tools/microbench/gather_cal.hip), WRITE_SIZE x1"}
+if sys.argv[4] == "20" and sys.argv[3] == "ches":
+    n, h, nb = 1 << 20, 12, 961017
+    out["decomposition_bytes"] = {
+        "table_rows_128B_lines": n * h * 128,          # 112-B internal rows padded to one 128-B line
+        "table_rows_blst_96B_algorithmic": n * h * 96,
+        "sorted_payload_4B": n * h * 4,
+        "bucket_meta_order_counts_offsets": nb * 12,
+        "bucket_xyzz_writes_224B": nb * 224,
+        "note": "counts[id]/offsets[id] are random 4-B reads and each bucket's payload run spans 1-2 lines: at "
+                "line granularity these add up to ~0.4 GB more; the rest of the FETCH excess is uncalibrated "
+                "(small random reads)"}
+if len(sys.argv) > 6:
+    out["calibration"] = json.load(open(sys.argv[6]))
 js = json.dumps(out, indent=1)
 print(js)
-if len(sys.argv) > 4:
-    open(sys.argv[4], "w").write(js + "\n")
+if len(sys.argv) > 5:
+    open(sys.argv[5], "w").write(js + "\n")
