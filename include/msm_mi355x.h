@@ -188,6 +188,18 @@ int msm_ches_params(int n_exp, int beta, int out[9]);
 int msm_ches_ctx_create(msm_ches_ctx **ctx, int group, int device, int n_exp, int beta);
 /* explicit parameters (same 9-int layout; b_size 0 = not checked) */
 int msm_ches_ctx_create_params(msm_ches_ctx **ctx, int group, int device, const int params[9]);
+/* One MSM over several devices from one process (the reference is
+ * single-device, its Go binding splits points x windows over CPU threads,
+ * bindings/go/blst.go:2064-2197).  The points are split into ndev contiguous
+ * balanced shards, shard g on devices[g] with its own rows of the reference
+ * table (the rows of point i are contiguous in main_p1.cpp:155-172's layout, so
+ * set/get/save/load_table keep that layout); each mult runs every shard
+ * concurrently and folds the 144/288-B partials exactly on the host.  n_exp /
+ * beta select the configuration of ONE SHARD (e.g. 2^21 points over 8 devices:
+ * n_exp = 18).  Devices may repeat (several shards on one device).  Points,
+ * table rows and scalars must be in host memory when ndev > 1. */
+int msm_ches_ctx_create_multi(msm_ches_ctx **ctx, int group, const int *devices, int ndev, int n_exp, int beta);
+int msm_ches_ctx_shards(const msm_ches_ctx *ctx);
 /* base points P_i (blst affine) -> T built on the GPU */
 int msm_ches_ctx_build_table(msm_ches_ctx *ctx, const void *points_affine, size_t npoints, int on_device,
                              void *hip_stream);

@@ -56,6 +56,8 @@ def lib():
     L.msm_ches_params.argtypes = [i32, i32, vp]
     L.msm_ches_ctx_create.argtypes = [pp, i32, i32, i32, i32]
     L.msm_ches_ctx_create_params.argtypes = [pp, i32, i32, vp]
+    L.msm_ches_ctx_create_multi.argtypes = [pp, i32, vp, i32, i32, i32]
+    L.msm_ches_ctx_shards.argtypes = [vp]
     L.msm_ches_ctx_build_table.argtypes = [vp, vp, sz, i32, vp]
     L.msm_ches_ctx_set_table.argtypes = [vp, vp, sz, i32, vp]
     L.msm_ches_ctx_get_table.argtypes = [vp, vp, sz, sz]

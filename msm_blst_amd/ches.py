@@ -51,13 +51,20 @@ class CHESContext:
     """One GPU, one point set, one CHES configuration.
 
     group: 1 (G1) or 2 (G2); n_exp/beta select the reference configuration, or
-    pass `p` (a dict with PARAM_KEYS) for explicit parameters.
+    pass `p` (a dict with PARAM_KEYS) for explicit parameters.  `devices` (a list
+    of device ids, repeats allowed) shards the points over several devices in
+    this process (msm_ches_ctx_create_multi); n_exp is then one shard's
+    configuration and points/tables/scalars are passed in host memory.
     """
 
-    def __init__(self, group=1, device=0, n_exp=None, beta=0, p=None):
+    def __init__(self, group=1, device=0, n_exp=None, beta=0, p=None, devices=None):
         self.group = group
         self._ctx = ctypes.c_void_p()
-        if p is None:
+        if devices is not None:
+            arr = (ctypes.c_int * len(devices))(*devices)
+            check(lib().msm_ches_ctx_create_multi(ctypes.byref(self._ctx), group, arr, len(devices), n_exp, beta))
+            self.params = params(n_exp, beta)
+        elif p is None:
             check(lib().msm_ches_ctx_create(ctypes.byref(self._ctx), group, device, n_exp, beta))
             self.params = params(n_exp, beta)
         else:
@@ -117,6 +124,9 @@ class CHESContext:
         raw = bytes(rets)
         nb = JAC_BYTES[self.group]
         return [raw[k * nb:(k + 1) * nb] for k in range(count)]
+
+    def shards(self):
+        return lib().msm_ches_ctx_shards(self._ctx)
 
     def bucket_count(self):
         return lib().msm_ches_ctx_bucket_count(self._ctx)

@@ -17,6 +17,7 @@
 
 #include "../../include/msm_mi355x.h"
 #include "engine.hpp"
+#include "multi.hpp"
 
 using namespace msm;
 
@@ -273,11 +274,10 @@ void fixed_points(hfp::Aff<F> *out, size_t n, hfp::Jac<F> g) {
 
 struct msm_ches_ctx {
   int group = 1;
-  int device = 0;
+  int device = 0;      // first shard's device
   bool ready = false;  // a table was built / set / loaded (mult before that: MSM_E_STATE)
-  std::unique_ptr<Ches<1>> g1;
-  std::unique_ptr<Ches<2>> g2;
-  DevBuf scalars;
+  std::unique_ptr<ChesMulti<1>> g1;  // one shard per device (multi.hpp); one shard = one device
+  std::unique_ptr<ChesMulti<2>> g2;
 };
 
 struct msm_bgmw_ctx {
@@ -650,8 +650,9 @@ int msm_ches_ctx_create_params(msm_ches_ctx **ctx, int group, int device, const 
     auto c = std::make_unique<msm_ches_ctx>();
     c->group = group;
     c->device = device;
-    if (group == 1) c->g1 = std::make_unique<Ches<1>>(device, p);
-    else c->g2 = std::make_unique<Ches<2>>(device, p);
+    const std::vector<int> devs{device};
+    if (group == 1) c->g1 = std::make_unique<ChesMulti<1>>(devs, p);
+    else c->g2 = std::make_unique<ChesMulti<2>>(devs, p);
     *ctx = c.release();
     return MSM_OK;
   } catch (const std::exception &e) {
@@ -664,6 +665,34 @@ int msm_ches_ctx_create(msm_ches_ctx **ctx, int group, int device, int n_exp, in
   int rc = msm_ches_params(n_exp, beta, v);
   if (rc) return rc;
   return msm_ches_ctx_create_params(ctx, group, device, v);
+}
+
+int msm_ches_ctx_create_multi(msm_ches_ctx **ctx, int group, const int *devices, int ndev, int n_exp, int beta) {
+  if (!ctx || !devices || ndev < 1 || (group != 1 && group != 2)) return fail(MSM_E_ARG, "bad ctx/group/devices");
+  int v[9];
+  int rc = msm_ches_params(n_exp, beta, v);
+  if (rc) return rc;
+  const int have = msm_device_count();
+  std::vector<int> devs(devices, devices + ndev);
+  for (int d : devs)
+    if (d < 0 || d >= have) return fail(MSM_E_NODEV, "no such HIP device");
+  ChesParams p{v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], v[8]};
+  try {
+    auto c = std::make_unique<msm_ches_ctx>();
+    c->group = group;
+    c->device = devs[0];
+    if (group == 1) c->g1 = std::make_unique<ChesMulti<1>>(devs, p);
+    else c->g2 = std::make_unique<ChesMulti<2>>(devs, p);
+    *ctx = c.release();
+    return MSM_OK;
+  } catch (const std::exception &e) {
+    return fail(MSM_E_HIP, e.what());
+  }
+}
+
+int msm_ches_ctx_shards(const msm_ches_ctx *ctx) {
+  if (!ctx) return 0;
+  return (int)(ctx->group == 1 ? ctx->g1->nshards() : ctx->g2->nshards());
 }
 
 #define CHES_DISPATCH(ctx, CALL) ((ctx)->group == 1 ? (ctx)->g1->CALL : (ctx)->g2->CALL)
@@ -709,20 +738,13 @@ int msm_ches_ctx_mult(msm_ches_ctx *ctx, void *ret, const byte *scalars, size_t 
   try {
     DeviceGuard g(ctx->device);
     hipStream_t s = (hipStream_t)stream;
-    size_t n = CHES_DISPATCH(ctx, npoints());
-    const uint8_t *d = scalars;
-    if (!on_device && n) {
-      ctx->scalars.ensure(n * stride + 16);
-      MSM_HIP_CHECK(hipMemcpyAsync(ctx->scalars.p, scalars, n * stride, hipMemcpyHostToDevice, s));
-      d = ctx->scalars.as<uint8_t>();
-    }
     if (ctx->group == 1) {
       hfp::Jac<hfp::Fp> out;
-      ctx->g1->run(s, d, stride, &out);
+      ctx->g1->run(s, scalars, stride, on_device != 0, &out);
       memcpy(ret, &out, sizeof out);
     } else {
       hfp::Jac<hfp::Fp2> out;
-      ctx->g2->run(s, d, stride, &out);
+      ctx->g2->run(s, scalars, stride, on_device != 0, &out);
       memcpy(ret, &out, sizeof out);
     }
     return MSM_OK;
@@ -763,13 +785,13 @@ int msm_ches_ctx_set_profiling(msm_ches_ctx *ctx, int on) {
 
 int msm_ches_ctx_phase_times(const msm_ches_ctx *ctx, float out[6]) {
   if (!ctx || !out) return fail(MSM_E_ARG, "null");
-  const PhaseTimes &t = CHES_DISPATCH(ctx, times());
+  const PhaseTimes &t = CHES_DISPATCH(ctx, front().times());
   const float v[6] = {t.digits, t.sort, t.accumulate, t.reduce, t.finalize, t.total};
   memcpy(out, v, sizeof v);
   return MSM_OK;
 }
 
-size_t msm_ches_ctx_bucket_count(const msm_ches_ctx *ctx) { return ctx ? CHES_DISPATCH(ctx, bucket_count()) : 0; }
+size_t msm_ches_ctx_bucket_count(const msm_ches_ctx *ctx) { return ctx ? CHES_DISPATCH(ctx, front().bucket_count()) : 0; }
 
 void msm_ches_ctx_destroy(msm_ches_ctx *ctx) { delete ctx; }
 

@@ -1,0 +1,223 @@
+// multi.hpp -- one CHES MSM over several MI355X devices from ONE process
+// (the C/C++ multi-device path behind msm_ches_ctx_create_multi).
+//
+// MSM is linear: Q = sum_g Q_g with Q_g = sum_{i in shard g} s_i P_i (SURVEY
+// 8e).  The n points are split into contiguous, balanced shards, one Ches<G>
+// engine per shard on its device; shard g builds (or receives) only its own
+// rows of the reference table T[3(i h + j) + m - 1] (main_p1.cpp:155-172: the
+// rows of point i are contiguous, so shard g's rows are one contiguous range of
+// the reference layout).  A multiplication runs every shard's MSM concurrently
+// (one host thread per shard, each driving its own device), and the single
+// exchange is the read-back of the shards' 144/288-B Jacobian partials, folded
+// on the host with an exact add (hfp::addj, doubling aware) in shard order.
+// No device-to-device traffic is needed: the partials reach host memory with
+// the per-MSM read-back every shard does anyway, so a collective (RCCL) would
+// only add a hop for 144 bytes.  The reference itself is single-device; its Go
+// binding splits points x windows over threads (bindings/go/blst.go:2064-2197),
+// which would replicate points and tables on every GPU, so points are sharded.
+//
+// Shards may share a device (devices = {0, 0, ...}): each engine keeps its own
+// buffers and streams, which is how the 1-GPU tests exercise the 8-shard fold.
+#pragma once
+#include <cstring>
+#include <exception>
+#include <memory>
+#include <thread>
+#include <vector>
+
+#include "engine.hpp"
+
+namespace msm {
+
+template <int G>
+class ChesMulti {
+ public:
+  typedef typename HostField<G>::F HF;
+  struct Shard {
+    int device = 0;
+    size_t start = 0, n = 0;  // global point range [start, start + n)
+    std::unique_ptr<Ches<G>> eng;
+    DevBuf scal;               // host scalars of this shard, per call
+    hipStream_t stream = nullptr;  // the shard's own stream (shards may share a device)
+  };
+
+  ChesMulti(const std::vector<int> &devices, const ChesParams &p) : p_(p) {
+    if (devices.empty()) throw std::runtime_error("ChesMulti: no devices");
+    shards_.resize(devices.size());
+    for (size_t g = 0; g < devices.size(); ++g) {
+      Shard &s = shards_[g];
+      s.device = devices[g];
+      s.eng = std::make_unique<Ches<G>>(s.device, p);
+      if (devices.size() > 1) {
+        DeviceGuard dg(s.device);
+        MSM_HIP_CHECK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+      }
+    }
+  }
+  ~ChesMulti() {
+    for (Shard &s : shards_)
+      if (s.stream) {
+        DeviceGuard dg(s.device);
+        (void)hipStreamSynchronize(s.stream);
+        (void)hipStreamDestroy(s.stream);
+      }
+  }
+  ChesMulti(const ChesMulti &) = delete;
+  ChesMulti &operator=(const ChesMulti &) = delete;
+  size_t nshards() const { return shards_.size(); }
+  const Shard &shard(size_t k) const { return shards_[k]; }
+  Ches<G> &front() { return *shards_[0].eng; }
+  const Ches<G> &front() const { return *shards_[0].eng; }
+  const ChesParams &params() const { return p_; }
+  size_t npoints() const { return n_; }
+  size_t rows_per_point() const { return 3 * (size_t)p_.h; }
+  size_t table_rows() const { return rows_per_point() * n_; }
+
+  // points: n blst affine points (host memory, or device memory of the single
+  // shard's device) -> every shard builds its rows on its own device
+  void build_table(const void *pts, size_t n, bool on_device, hipStream_t s) {
+    split(n);
+    if (shards_.size() == 1) {
+      shards_[0].eng->build_table(pts, n, on_device, s);
+      return;
+    }
+    if (on_device) throw std::runtime_error("multi-device build_table takes host points");
+    const uint8_t *P = static_cast<const uint8_t *>(pts);
+    each([&](Shard &sh) { sh.eng->build_table(P + sh.start * 96 * G, sh.n, false, sh.stream); });
+  }
+  void reserve_table(size_t n) {
+    split(n);
+    for (Shard &sh : shards_) sh.eng->reserve_table(sh.n);
+  }
+  // reference-layout rows [first, first + count) -> the shards that own them
+  void put_table(const void *rows, size_t first, size_t count, bool on_device, hipStream_t s) {
+    if (shards_.size() == 1) return shards_[0].eng->put_table(rows, first, count, on_device, s);
+    if (on_device) throw std::runtime_error("multi-device put_table takes host rows");
+    route(first, count, [&](Shard &sh, size_t r0, size_t cnt, size_t off) {
+      sh.eng->put_table(static_cast<const uint8_t *>(rows) + off * 96 * G, r0, cnt, false, sh.stream);
+    });
+  }
+  void set_table(const void *tab, size_t n, bool on_device, hipStream_t s) {
+    reserve_table(n);
+    put_table(tab, 0, table_rows(), on_device, s);
+  }
+  void get_table(void *out, size_t first, size_t count, hipStream_t s) {
+    if (first + count > table_rows()) throw std::runtime_error("table range out of bounds");
+    if (shards_.size() == 1) return shards_[0].eng->get_table(out, first, count, s);
+    route(first, count, [&](Shard &sh, size_t r0, size_t cnt, size_t off) {
+      sh.eng->get_table(static_cast<uint8_t *>(out) + off * 96 * G, r0, cnt, sh.stream);
+    });
+  }
+
+  // scalars: n strings of `stride` bytes (host memory; device memory only for a
+  // single shard, on its device)
+  void run(hipStream_t s, const uint8_t *scalars, size_t stride, bool on_device, hfp::Jac<HF> *out) {
+    if (shards_.size() == 1) {
+      Shard &sh = shards_[0];
+      const uint8_t *d = scalars;
+      if (!on_device && sh.n) {
+        DeviceGuard g(sh.device);
+        sh.scal.ensure(sh.n * stride + 16);
+        MSM_HIP_CHECK(hipMemcpyAsync(sh.scal.p, scalars, sh.n * stride, hipMemcpyHostToDevice, s));
+        d = static_cast<const uint8_t *>(sh.scal.p);
+      }
+      sh.eng->run(s, d, stride, out);
+      return;
+    }
+    if (on_device) throw std::runtime_error("multi-device mult takes host scalars");
+    std::vector<hfp::Jac<HF>> part(shards_.size());
+    each([&](Shard &sh) {
+      DeviceGuard g(sh.device);
+      hfp::Jac<HF> r;
+      if (sh.n) {
+        sh.scal.ensure(sh.n * stride + 16);
+        MSM_HIP_CHECK(hipMemcpyAsync(sh.scal.p, scalars + sh.start * stride, sh.n * stride, hipMemcpyHostToDevice,
+                                     sh.stream));
+        sh.eng->run(sh.stream, static_cast<const uint8_t *>(sh.scal.p), stride, &r);
+      } else {
+        std::memset(&r, 0, sizeof r);
+      }
+      part[&sh - shards_.data()] = r;
+    });
+    *out = fold(part);
+  }
+
+  // count MSMs: scalar set k at scalars + k * set_stride (host memory for
+  // several shards); every shard runs its own pipelined batch on its slice
+  void run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, size_t set_stride, size_t count,
+                 hfp::Jac<HF> *outs, bool on_host) {
+    if (shards_.size() == 1) return shards_[0].eng->run_batch(s, scalars, stride, set_stride, count, outs, on_host);
+    if (!on_host) throw std::runtime_error("multi-device mult_batch takes host scalars");
+    std::vector<std::vector<hfp::Jac<HF>>> part(shards_.size(), std::vector<hfp::Jac<HF>>(count));
+    each([&](Shard &sh) {
+      std::vector<hfp::Jac<HF>> &r = part[&sh - shards_.data()];
+      if (sh.n) {
+        DeviceGuard g(sh.device);
+        sh.eng->run_batch(sh.stream, scalars + sh.start * stride, stride, set_stride, count, r.data(), true);
+        MSM_HIP_CHECK(hipStreamSynchronize(sh.stream));
+      } else {
+        for (auto &j : r) std::memset(&j, 0, sizeof j);
+      }
+    });
+    for (size_t k = 0; k < count; ++k) {
+      std::vector<hfp::Jac<HF>> col(shards_.size());
+      for (size_t g = 0; g < shards_.size(); ++g) col[g] = part[g][k];
+      outs[k] = fold(col);
+    }
+  }
+
+  void set_profiling(bool on) {
+    for (Shard &sh : shards_) sh.eng->set_profiling(on);
+  }
+
+ private:
+  ChesParams p_;
+  std::vector<Shard> shards_;
+  size_t n_ = 0;
+
+  void split(size_t n) {
+    const size_t S = shards_.size(), base = n / S, rem = n % S;
+    size_t at = 0;
+    for (size_t g = 0; g < S; ++g) {
+      shards_[g].start = at;
+      shards_[g].n = base + (g < rem ? 1 : 0);
+      at += shards_[g].n;
+    }
+    n_ = n;
+  }
+  // run f on every shard, one host thread each; the first exception is rethrown
+  template <class Fn>
+  void each(Fn f) {
+    std::vector<std::exception_ptr> err(shards_.size());
+    std::vector<std::thread> th;
+    for (size_t g = 0; g < shards_.size(); ++g)
+      th.emplace_back([&, g] {
+        try {
+          f(shards_[g]);
+        } catch (...) {
+          err[g] = std::current_exception();
+        }
+      });
+    for (auto &t : th) t.join();
+    for (auto &e : err)
+      if (e) std::rethrow_exception(e);
+  }
+  // split a reference-layout row range over the owning shards:
+  // f(shard, first row within the shard, rows, offset into the caller's range)
+  template <class Fn>
+  void route(size_t first, size_t count, Fn f) {
+    const size_t R = rows_per_point();
+    for (Shard &sh : shards_) {
+      const size_t lo = sh.start * R, hi = (sh.start + sh.n) * R;
+      const size_t a = std::max(lo, first), b = std::min(hi, first + count);
+      if (a < b) f(sh, a - lo, b - a, a - first);
+    }
+  }
+  static hfp::Jac<HF> fold(const std::vector<hfp::Jac<HF>> &part) {
+    hfp::Jac<HF> acc = part[0];
+    for (size_t g = 1; g < part.size(); ++g) acc = hfp::addj(acc, part[g]);
+    return acc;
+  }
+};
+
+}  // namespace msm

@@ -4,6 +4,13 @@
 // the reference builds main_test_p1 / main_test_p2 (ref makefile:7-13).
 //
 //   ./msm_driver_p1 config=20 [beta=0] [device=0] [tests=5] [loops=N] [host_tables=0]
+//                  [gpus=N | devices=d0,d1,...]
+//
+// gpus= / devices= shard the CHES method's points over several devices of this
+// process (msm_ches_ctx_create_multi; devices may repeat): each shard uses the
+// reference configuration of its size, config - ceil(log2(shards)) (2^21 points
+// over 8 devices: config_file_n_exp_18.h per shard, BASELINE configs[3]); the
+// other three methods stay on `device`.
 //
 // mirrors `./run.sh group=1 config=20` (ref run.sh:1-42): builds the fixed
 // points, the CHES and BGMW95 tables (on the GPU), then test_pippengers().  The
@@ -42,6 +49,7 @@ msm_driver_affine *PRECOMPUTATION_POINTS_LIST_3nh = nullptr;
 msm_driver_affine *PRECOMPUTATION_POINTS_LIST_BGMW95 = nullptr;
 
 static int g_beta = 0, g_device = 0, g_host_tables = 0;
+static std::vector<int> g_devices;  // CHES shards (empty: one shard on g_device)
 static msm_ches_ctx *g_ches = nullptr;
 static msm_bgmw_ctx *g_bgmw = nullptr;
 
@@ -91,10 +99,22 @@ void init_pippenger_CHES_q_over_5() {
   check(msm_ches_digit_table(q, a_LEADING_TERM, DIGIT_CONVERSION_HASH_TABLE), "digit table");
   printf("DIGIT_CONVERSION_HASH_TABLE constructed.\n");
   auto st = std::chrono::steady_clock::now();
-  check(msm_ches_ctx_create(&g_ches, GROUP, g_device, N_EXP, g_beta), "msm_ches_ctx_create");
+  int h_table = h_LEN_SCALAR;
+  if (g_devices.size() > 1) {
+    int lg = 0;
+    while ((1u << lg) < g_devices.size()) ++lg;
+    int sp[9];
+    check(msm_ches_params(N_EXP - lg, g_beta, sp), "per-shard CHES configuration");
+    h_table = sp[3];
+    check(msm_ches_ctx_create_multi(&g_ches, GROUP, g_devices.data(), (int)g_devices.size(), N_EXP - lg, g_beta),
+          "msm_ches_ctx_create_multi");
+    printf("CHES sharded over %zu devices, config_file_n_exp_%d per shard\n", g_devices.size(), N_EXP - lg);
+  } else {
+    check(msm_ches_ctx_create(&g_ches, GROUP, g_device, N_EXP, g_beta), "msm_ches_ctx_create");
+  }
   check(msm_ches_ctx_build_table(g_ches, FIX_POINTS_LIST, N_POINTS, 0, nullptr), "CHES table");
   if (g_host_tables) {
-    const size_t cnt = 3 * N_POINTS * (size_t)h_LEN_SCALAR;
+    const size_t cnt = 3 * N_POINTS * (size_t)h_table;
     PRECOMPUTATION_POINTS_LIST_3nh = new msm_driver_affine[cnt];
     check(msm_ches_ctx_get_table(g_ches, PRECOMPUTATION_POINTS_LIST_3nh, 0, cnt), "CHES table read-back");
   }
@@ -262,8 +282,20 @@ int main(int argc, char **argv) {
     else if (!strncmp(s, "tests=", 6)) g_tests = atoi(s + 6);
     else if (!strncmp(s, "loops=", 6)) g_loops = atoi(s + 6);
     else if (!strncmp(s, "host_tables=", 12)) host_tables = atoi(s + 12);
-    else {
-      fprintf(stderr, "usage: %s config=<n_exp 8..21> [beta=0|1] [device=0] [tests=5] [loops=N] [host_tables=0|1]\n",
+    else if (!strncmp(s, "gpus=", 5)) {
+      g_devices.clear();
+      for (int d = 0; d < atoi(s + 5); ++d) g_devices.push_back(d);
+    } else if (!strncmp(s, "devices=", 8)) {
+      g_devices.clear();
+      for (const char *c = s + 8; *c;) {
+        g_devices.push_back(atoi(c));
+        while (*c && *c != ',') ++c;
+        if (*c == ',') ++c;
+      }
+    } else {
+      fprintf(stderr,
+              "usage: %s config=<n_exp 8..21> [beta=0|1] [device=0] [tests=5] [loops=N] [host_tables=0|1] "
+              "[gpus=N | devices=d0,d1,...]\n",
               argv[0]);
       return 2;
     }
@@ -276,6 +308,11 @@ int main(int argc, char **argv) {
     fprintf(stderr, "no HIP device %d visible\n", device);
     return 2;
   }
+  for (int d : g_devices)
+    if (d < 0 || d >= msm_device_count()) {
+      fprintf(stderr, "no HIP device %d visible\n", d);
+      return 2;
+    }
   init_fix_point_list();
   init_pippenger_CHES_q_over_5();
   init_pippenger_BGMW95();

@@ -62,6 +62,18 @@ __global__ __launch_bounds__(256) void k_rate(uint32_t *out, uint32_t seed) {
         uint32_t x = (uint32_t)acc[k];
         asm volatile("v_add_u32 %0, %0, %1" : "+v"(x) : "v"(a[k]));
         acc[k] = x;
+      } else if constexpr (KIND == 12) {  // v_lshrrev_b64 (the FIPS column carry shift)
+        asm volatile("v_lshrrev_b64 %0, 28, %0" : "+v"(acc[k]));
+      } else if constexpr (KIND == 13) {  // v_and_b32
+        uint32_t x = (uint32_t)acc[k];
+        asm volatile("v_and_b32 %0, %0, %1" : "+v"(x) : "v"(a[k]));
+        acc[k] = x;
+      } else if constexpr (KIND == 14) {  // v_alignbit_b32 (one half of a 64-bit shift)
+        uint32_t x = (uint32_t)acc[k];
+        asm volatile("v_alignbit_b32 %0, %1, %0, 28" : "+v"(x) : "v"(a[k]));
+        acc[k] = x;
+      } else if constexpr (KIND == 15) {  // v_mad_u64_u32 with a zero addend (a 32x32->64 multiply)
+        asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(acc[k]) : "v"((uint32_t)acc[k]), "v"(b) : "vcc");
       }
     }
   }
@@ -72,7 +84,8 @@ __global__ __launch_bounds__(256) void k_rate(uint32_t *out, uint32_t seed) {
 }
 
 static const char *names[] = {"v_mad_u64_u32(vcc)", "v_mul_lo_u32", "v_mul_hi_u32", "v_add_co+v_addc_co (pair)", "v_fma_f64",
-                              "v_mad_u32_u24", "v_add3_u32", "v_mul_hi_u32_u24", "v_add_co_u32", "v_mad_u64_u32(sgpr)", "v_lshl_add_u64", "v_add_u32"};
+                              "v_mad_u32_u24", "v_add3_u32", "v_mul_hi_u32_u24", "v_add_co_u32", "v_mad_u64_u32(sgpr)", "v_lshl_add_u64", "v_add_u32",
+                              "v_lshrrev_b64", "v_and_b32", "v_alignbit_b32", "v_mad_u64_u32(x,y,0)"};
 
 template <int K>
 void run(uint32_t *d_out, int blocks) {
@@ -99,7 +112,8 @@ int main() {
   hipMalloc(&d_out, (size_t)blocks * 256 * 4);
   run<0>(d_out, blocks); run<9>(d_out, blocks); run<1>(d_out, blocks); run<2>(d_out, blocks); run<3>(d_out, blocks);
   run<4>(d_out, blocks); run<5>(d_out, blocks); run<6>(d_out, blocks); run<7>(d_out, blocks); run<8>(d_out, blocks);
-  run<10>(d_out, blocks); run<11>(d_out, blocks);
+  run<10>(d_out, blocks); run<11>(d_out, blocks); run<12>(d_out, blocks); run<13>(d_out, blocks);
+  run<14>(d_out, blocks); run<15>(d_out, blocks);
   hipFree(d_out);
   return 0;
 }
