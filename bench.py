@@ -59,8 +59,8 @@ class Bracket:
     """W untimed warmup already done by the caller; barrier + synchronize on both
     sides of the timed region, max over ranks."""
 
-    def __init__(self, world, dev):
-        self.world, self.dev = world, dev
+    def __init__(self, world, dev, xdev=None):
+        self.world, self.dev, self.xdev = world, dev, xdev
 
     def __enter__(self):
         import torch
@@ -77,7 +77,7 @@ class Bracket:
             torch.distributed.barrier()
         el = time.perf_counter() - self.t
         if self.world > 1:
-            t = torch.tensor([el], dtype=torch.float64, device=self.dev)
+            t = torch.tensor([el], dtype=torch.float64, device=self.xdev)
             torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
             el = float(t.item())
         self.elapsed = el
@@ -126,6 +126,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-log-n", type=int, default=20)
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="nccl = RCCL over xGMI (the multi-GPU bench); gloo only for --one-device rehearsals")
+    ap.add_argument("--one-device", action="store_true",
+                    help="rehearsal on a 1-GPU box: every rank uses device 0 (with --dist-backend gloo)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -135,11 +139,17 @@ def main():
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
 
     import torch
+    if args.one_device:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    xdev = dev if args.dist_backend == "nccl" else None  # where exchanged tensors live
 
     import msm_blst_amd as m
     from msm_blst_amd import dist as mdist
@@ -163,7 +173,7 @@ def main():
     def fold_all(parts):
         if world == 1:
             return parts
-        return [mdist.fold(ps, add) for ps in mdist.gather_partials_batch(parts, G, dev)]
+        return [mdist.fold(ps, add) for ps in mdist.gather_partials_batch(parts, G, xdev)]
 
     def make(method):
         t = time.time()
@@ -190,10 +200,10 @@ def main():
     def sync_steps(mult, k_steps, on_device):
         """k_steps synchronous MSMs over sets 0..k_steps-1 (exchange + fold per step)."""
         out = []
-        with Bracket(world, dev) as b:
+        with Bracket(world, dev, xdev) as b:
             for k in range(k_steps):
                 part = mult(k, on_device)
-                out.append(part if world == 1 else mdist.fold(mdist.gather_partials(part, G, dev), add))
+                out.append(part if world == 1 else mdist.fold(mdist.gather_partials(part, G, xdev), add))
         return out, b.elapsed
 
     ctx, mult = make(args.method)
@@ -202,7 +212,7 @@ def main():
     if batched:
         if W:
             ctx.mult_batch(hptr, min(W, K), 32, set_stride=SS, on_device=False, stream=sp)
-        with Bracket(world, dev) as b:  # headline: host scalars, H2D inside the pipeline
+        with Bracket(world, dev, xdev) as b:  # headline: host scalars, H2D inside the pipeline
             parts = ctx.mult_batch(hptr, K, 32, set_stride=SS, on_device=False, stream=sp)
             res = fold_all(parts)
         elapsed, acc_ms = b.elapsed, ctx.phase_times()["accumulate"]
@@ -210,7 +220,7 @@ def main():
                                   "kernel_ms": round(acc_ms, 4),
                                   "note": "headline: K distinct scalar sets in pinned host memory, H2D in the timed region"}
         if not args.no_compare:
-            with Bracket(world, dev) as b:
+            with Bracket(world, dev, xdev) as b:
                 rparts = fold_all(ctx.mult_batch(dptr, K, 32, set_stride=SS, on_device=True, stream=sp))
             legs["ches_batch_resident"] = {"value": round(n * world * K / b.elapsed, 1),
                                            "ms_per_step": round(b.elapsed / K * 1e3, 4),
@@ -246,7 +256,7 @@ def main():
         pctx.set_points(pts, n, stream=sp)
         pp = pctx.mult(dptr, 255, stride=32, on_device=True, stream=sp)
         mine = ctx.mult(dptr, 32, on_device=True, stream=sp) if args.method != "pippenger" else pp
-        cross = all_true(m.compress(G, pp) == m.compress(G, mine), world, dev)
+        cross = all_true(m.compress(G, pp) == m.compress(G, mine), world, xdev)
         pctx.close()
 
     others = {}
