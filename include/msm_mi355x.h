@@ -147,6 +147,30 @@ void blst_p2_tile_pippenger_BGMW95(blst_p2 *ret, const blst_p2_affine *const poi
 void blst_p1s_add(blst_p1 *ret, const blst_p1_affine *const points[], size_t npoints);
 void blst_p2s_add(blst_p2 *ret, const blst_p2_affine *const points[], size_t npoints);
 
+/* ---- fixed-window MSM with a precomputed table (replaces ref src/multi_scalar.c:63-261,
+ * blst.h:228-236 and :367-375; used by the C++ binding's P1_Affines / P2_Affines,
+ * ref bindings/blst.hpp:362-430) ----
+ * Same semantics and table layout as blst: table row i holds the canonical affine
+ * multiples (k+1) P_i, k < 2^(wbits-1), wbits in [2, 14]; precompute may be called
+ * with the points stored inside the output table (blst.hpp:383-393); the pointer
+ * rules of blst apply to points[] and scalars[] (stride (nbits+7)/8).  On the GPU:
+ * precompute builds every row by repeated mixed additions and one batch inversion
+ * per point; mult sums the Booth-digit gathers of each window in parallel and
+ * combines the window totals on the host.  The table is uploaded on every mult
+ * call (the msm_wbits_ctx_* API below keeps it resident).  scratch is not used. */
+size_t blst_p1s_mult_wbits_precompute_sizeof(size_t wbits, size_t npoints);
+void blst_p1s_mult_wbits_precompute(blst_p1_affine table[], size_t wbits, const blst_p1_affine *const points[],
+                                    size_t npoints);
+size_t blst_p1s_mult_wbits_scratch_sizeof(size_t npoints);
+void blst_p1s_mult_wbits(blst_p1 *ret, const blst_p1_affine table[], size_t wbits, size_t npoints,
+                         const byte *const scalars[], size_t nbits, limb_t *scratch);
+size_t blst_p2s_mult_wbits_precompute_sizeof(size_t wbits, size_t npoints);
+void blst_p2s_mult_wbits_precompute(blst_p2_affine table[], size_t wbits, const blst_p2_affine *const points[],
+                                    size_t npoints);
+size_t blst_p2s_mult_wbits_scratch_sizeof(size_t npoints);
+void blst_p2s_mult_wbits(blst_p2 *ret, const blst_p2_affine table[], size_t wbits, size_t npoints,
+                         const byte *const scalars[], size_t nbits, limb_t *scratch);
+
 /* ---- extension API: device-resident contexts (points uploaded once) ---- */
 enum {
   MSM_OK = 0,
@@ -254,6 +278,22 @@ int msm_bgmw_ctx_set_profiling(msm_bgmw_ctx *ctx, int on);
 int msm_bgmw_ctx_phase_times(const msm_bgmw_ctx *ctx, float out[6]);
 size_t msm_bgmw_ctx_bucket_count(const msm_bgmw_ctx *ctx);
 void msm_bgmw_ctx_destroy(msm_bgmw_ctx *ctx);
+
+/* ---- fixed-window (wbits) MSM with the table resident in HBM ---- */
+typedef struct msm_wbits_ctx msm_wbits_ctx;
+int msm_wbits_ctx_create(msm_wbits_ctx **ctx, int group, int device, int wbits);
+/* base points (blst affine, host or device) -> the table, built on the GPU */
+int msm_wbits_ctx_precompute(msm_wbits_ctx *ctx, const void *points_affine, size_t npoints, int on_device,
+                             void *hip_stream);
+/* a table in the reference layout (npoints << (wbits-1) blst affine rows), host or device */
+int msm_wbits_ctx_set_table(msm_wbits_ctx *ctx, const void *table_affine, size_t npoints, int on_device,
+                            void *hip_stream);
+int msm_wbits_ctx_get_table(msm_wbits_ctx *ctx, void *out_affine, size_t first, size_t count);
+/* scalars: npoints LE strings of `stride` bytes (>= (nbits+7)/8), host or device; low nbits bits */
+int msm_wbits_ctx_mult(msm_wbits_ctx *ctx, void *ret, const byte *scalars, size_t stride, size_t nbits,
+                       int scalars_on_device, void *hip_stream);
+size_t msm_wbits_ctx_table_rows(const msm_wbits_ctx *ctx);
+void msm_wbits_ctx_destroy(msm_wbits_ctx *ctx);
 
 /* host setup logic of the CHES method (no device work):
  * bucket set of ref auxiliaryfunc.h:257-288 (returns |B|; out may be NULL) */

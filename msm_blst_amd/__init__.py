@@ -10,14 +10,16 @@ Mirrors:
   MSMContext                                          device-resident points (extension)
   ches.CHESContext                                    ref main_p1.cpp CHES driver (see ches.py)
   bgmw.BGMWContext                                    ref main_p1.cpp BGMW95 driver (see bgmw.py)
+  wbits.WbitsContext, wbits.precompute / wbits.mult   blst_p{1,2}s_mult_wbits[_precompute] (see wbits.py)
 """
 import ctypes
 
 from ._ffi import MsmError, check, lib
 from .bgmw import BGMWContext
 from .ches import CHESContext
+from .wbits import WbitsContext
 
-__all__ = ["MsmError", "MSMContext", "CHESContext", "BGMWContext", "p1s_mult_pippenger", "p2s_mult_pippenger", "ps_add", "fixed_points", "gen_scalars",
+__all__ = ["MsmError", "MSMContext", "CHESContext", "BGMWContext", "WbitsContext", "p1s_mult_pippenger", "p2s_mult_pippenger", "ps_add", "fixed_points", "gen_scalars",
            "compress", "to_affine", "device_count", "lib"]
 
 POINT_BYTES = {1: 96, 2: 192}

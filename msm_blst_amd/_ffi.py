@@ -72,6 +72,24 @@ def lib():
     L.msm_ches_bucket_set.argtypes = [i32, i32, vp, sz]
     L.msm_ches_bucket_set.restype = sz
     L.msm_ches_digit_table.argtypes = [i32, i32, vp]
+    for g in (1, 2):
+        f = getattr(L, f"blst_p{g}s_mult_wbits_precompute_sizeof")
+        f.argtypes, f.restype = [sz, sz], sz
+        f = getattr(L, f"blst_p{g}s_mult_wbits_scratch_sizeof")
+        f.argtypes, f.restype = [sz], sz
+        f = getattr(L, f"blst_p{g}s_mult_wbits_precompute")
+        f.argtypes, f.restype = [vp, sz, vp, sz], None
+        f = getattr(L, f"blst_p{g}s_mult_wbits")
+        f.argtypes, f.restype = [vp, vp, sz, sz, vp, sz, vp], None
+    L.msm_wbits_ctx_create.argtypes = [pp, i32, i32, i32]
+    L.msm_wbits_ctx_precompute.argtypes = [vp, vp, sz, i32, vp]
+    L.msm_wbits_ctx_set_table.argtypes = [vp, vp, sz, i32, vp]
+    L.msm_wbits_ctx_get_table.argtypes = [vp, vp, sz, sz]
+    L.msm_wbits_ctx_mult.argtypes = [vp, vp, vp, sz, sz, i32, vp]
+    L.msm_wbits_ctx_table_rows.argtypes = [vp]
+    L.msm_wbits_ctx_table_rows.restype = sz
+    L.msm_wbits_ctx_destroy.argtypes = [vp]
+    L.msm_wbits_ctx_destroy.restype = None
     L.msm_bgmw_ctx_create.argtypes = [pp, i32, i32, i32, i32]
     L.msm_bgmw_ctx_build_table.argtypes = [vp, vp, sz, i32, vp]
     L.msm_bgmw_ctx_set_table.argtypes = [vp, vp, sz, i32, vp]

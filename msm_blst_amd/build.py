@@ -24,7 +24,7 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-
 # (source, MSM_GROUP or None): the group-templated engines compile once per
 # group in parallel (the G2 instantiations dominate the build time)
 SOURCES = [("engine.hip", 1), ("engine.hip", 2), ("ches.hip", 1), ("ches.hip", 2), ("bgmw.hip", 1), ("bgmw.hip", 2),
-           ("compat.hip", 1), ("compat.hip", 2),
+           ("compat.hip", 1), ("compat.hip", 2), ("wbits.hip", 1), ("wbits.hip", 2),
            ("abi.cpp", None)]
 
 

@@ -255,6 +255,62 @@ void points_add(void *ret, const void *const *points, size_t n) {
   entry_msm<G>(ret, flat.data(), n, keys.data(), vals.data(), n, nb, w.data(), nullptr);
 }
 
+// ---- fixed-window MSM with a precomputed table (ref multi_scalar.c:63-261) ----
+template <int G>
+Wbits<G> &tls_wbits(int wbits) {
+  thread_local std::map<std::pair<int, int>, std::unique_ptr<Wbits<G>>> engines;
+  int dev = 0;
+  MSM_HIP_CHECK(hipGetDevice(&dev));
+  auto key = std::make_pair(dev, wbits);
+  auto it = engines.find(key);
+  if (it == engines.end()) it = engines.emplace(key, std::make_unique<Wbits<G>>(dev, wbits)).first;
+  return *it->second;
+}
+
+// all points are read (pointer rule of ref multi_scalar.c:136: a NULL entry
+// continues after the previous point) before the table is written, so the
+// binding's in-place call (points at the end of the table, blst.hpp:383-393) works
+template <int G>
+void wbits_precompute(void *table, size_t wbits, const void *const *points, size_t n) {
+  const size_t psz = 96 * G;
+  std::vector<uint8_t> flat(n * psz);
+  const uint8_t *pt = nullptr;
+  for (size_t i = 0; i < n; ++i) {
+    pt = *points ? (const uint8_t *)*points++ : pt + psz;
+    memcpy(flat.data() + i * psz, pt, psz);
+  }
+  if (!n) return;
+  Wbits<G> &eng = tls_wbits<G>((int)wbits);
+  eng.precompute(flat.data(), n, false, (hipStream_t)0);
+  eng.get_table(table, 0, eng.table_rows(), (hipStream_t)0);
+}
+
+// scalar pointer rule of ref multi_scalar.c:165,191: the first pointer is
+// taken, then NULL continues after the previous scalar (stride (nbits+7)/8)
+template <int G>
+void wbits_mult(void *ret, const void *table, size_t wbits, size_t n, const byte *const *scalars, size_t nbits) {
+  typedef typename HostField<G>::F HF;
+  hfp::Jac<HF> out;
+  memset(&out, 0, sizeof out);
+  if (n && nbits) {
+    const size_t nb = (nbits + 7) / 8;
+    std::vector<uint8_t> sc(n * nb);
+    const uint8_t *s = *scalars++;
+    memcpy(sc.data(), s, nb);
+    for (size_t i = 1; i < n; ++i) {
+      s = *scalars ? *scalars++ : s + nb;
+      memcpy(sc.data() + i * nb, s, nb);
+    }
+    Wbits<G> &eng = tls_wbits<G>((int)wbits);
+    eng.set_table(table, n, false, (hipStream_t)0);
+    DevBuf d;
+    d.ensure(sc.size() + 16);
+    MSM_HIP_CHECK(hipMemcpy(d.p, sc.data(), sc.size(), hipMemcpyHostToDevice));
+    eng.run((hipStream_t)0, d.as<uint8_t>(), nb, (int)nbits, &out);
+  }
+  memcpy(ret, &out, sizeof out);
+}
+
 size_t blst_window(size_t n) {  // ref multi_scalar.c:268-275
   size_t w = 0;
   while (n >>= 1) ++w;
@@ -286,6 +342,15 @@ struct msm_bgmw_ctx {
   bool ready = false;
   std::unique_ptr<Bgmw<1>> g1;
   std::unique_ptr<Bgmw<2>> g2;
+  DevBuf scalars;
+};
+
+struct msm_wbits_ctx {
+  int group = 1;
+  int device = 0;
+  bool ready = false;
+  std::unique_ptr<Wbits<1>> g1;
+  std::unique_ptr<Wbits<2>> g2;
   DevBuf scalars;
 };
 
@@ -543,6 +608,35 @@ MSM_CHES_ENTRIES(2)
 MSM_POINTS_ADD(1)
 MSM_POINTS_ADD(2)
 #undef MSM_POINTS_ADD
+
+// ---- fixed-window MSM with a precomputed table (replaces ref multi_scalar.c:63-261) ----
+#define MSM_WBITS_ENTRIES(g, scratch_pts)                                                                         \
+  size_t blst_p##g##s_mult_wbits_precompute_sizeof(size_t wbits, size_t npoints) {                              \
+    return (sizeof(blst_p##g##_affine) * npoints) << (wbits - 1);                                                 \
+  }                                                                                                               \
+  void blst_p##g##s_mult_wbits_precompute(blst_p##g##_affine table[], size_t wbits,                              \
+                                          const blst_p##g##_affine *const points[], size_t npoints) {            \
+    try {                                                                                                         \
+      wbits_precompute<g>(table, wbits, (const void *const *)points, npoints);                                    \
+    } catch (const std::exception &e) {                                                                           \
+      die("blst_p" #g "s_mult_wbits_precompute", e);                                                              \
+    }                                                                                                             \
+  }                                                                                                               \
+  size_t blst_p##g##s_mult_wbits_scratch_sizeof(size_t npoints) {                                                \
+    return sizeof(blst_p##g) * (npoints < scratch_pts ? npoints : scratch_pts);                                   \
+  }                                                                                                               \
+  void blst_p##g##s_mult_wbits(blst_p##g *ret, const blst_p##g##_affine table[], size_t wbits, size_t npoints,   \
+                               const byte *const scalars[], size_t nbits, limb_t *scratch) {                      \
+    (void)scratch;                                                                                                \
+    try {                                                                                                         \
+      wbits_mult<g>(ret, table, wbits, npoints, scalars, nbits);                                                  \
+    } catch (const std::exception &e) {                                                                           \
+      die("blst_p" #g "s_mult_wbits", e);                                                                         \
+    }                                                                                                             \
+  }
+MSM_WBITS_ENTRIES(1, 8192)  /* SCRATCH_SZ of ref multi_scalar.c:78 */
+MSM_WBITS_ENTRIES(2, 4096)
+#undef MSM_WBITS_ENTRIES
 
 const char *msm_last_error(void) { return g_err.c_str(); }
 
@@ -1060,6 +1154,93 @@ int msm_test_xyzz(int group, const void *pts, size_t npts, const uint32_t *ops, 
     return fail(MSM_E_HIP, e.what());
   }
 }
+
+// ---------------- fixed-window (wbits) contexts ----------------
+#define WB_DISPATCH(ctx, CALL) ((ctx)->group == 1 ? (ctx)->g1->CALL : (ctx)->g2->CALL)
+
+int msm_wbits_ctx_create(msm_wbits_ctx **ctx, int group, int device, int wbits) {
+  if (!ctx || (group != 1 && group != 2)) return fail(MSM_E_ARG, "bad ctx/group");
+  if (msm_device_count() <= device || device < 0) return fail(MSM_E_NODEV, "no such HIP device");
+  try {
+    auto c = std::make_unique<msm_wbits_ctx>();
+    c->group = group;
+    c->device = device;
+    if (group == 1) c->g1 = std::make_unique<Wbits<1>>(device, wbits);
+    else c->g2 = std::make_unique<Wbits<2>>(device, wbits);
+    *ctx = c.release();
+    return MSM_OK;
+  } catch (const std::exception &e) {
+    return fail(MSM_E_ARG, e.what());
+  }
+}
+
+int msm_wbits_ctx_precompute(msm_wbits_ctx *ctx, const void *pts, size_t n, int on_device, void *stream) {
+  if (!ctx || (!pts && n)) return fail(MSM_E_ARG, "bad args");
+  try {
+    ctx->ready = false;
+    WB_DISPATCH(ctx, precompute(pts, n, on_device != 0, (hipStream_t)stream));
+    ctx->ready = true;
+    return MSM_OK;
+  } catch (const std::exception &e) {
+    return fail(MSM_E_HIP, e.what());
+  }
+}
+
+int msm_wbits_ctx_set_table(msm_wbits_ctx *ctx, const void *tab, size_t n, int on_device, void *stream) {
+  if (!ctx || (!tab && n)) return fail(MSM_E_ARG, "bad args");
+  try {
+    ctx->ready = false;
+    WB_DISPATCH(ctx, set_table(tab, n, on_device != 0, (hipStream_t)stream));
+    ctx->ready = true;
+    return MSM_OK;
+  } catch (const std::exception &e) {
+    return fail(MSM_E_HIP, e.what());
+  }
+}
+
+int msm_wbits_ctx_get_table(msm_wbits_ctx *ctx, void *out, size_t first, size_t count) {
+  if (!ctx || (!out && count)) return fail(MSM_E_ARG, "bad args");
+  try {
+    WB_DISPATCH(ctx, get_table(out, first, count, (hipStream_t)0));
+    return MSM_OK;
+  } catch (const std::exception &e) {
+    return fail(MSM_E_ARG, e.what());
+  }
+}
+
+int msm_wbits_ctx_mult(msm_wbits_ctx *ctx, void *ret, const byte *scalars, size_t stride, size_t nbits,
+                       int on_device, void *stream) {
+  if (!ctx || !ret || stride == 0 || (nbits + 7) / 8 > stride) return fail(MSM_E_ARG, "bad args (stride < nbits/8)");
+  if (!ctx->ready) return fail(MSM_E_STATE, "no table: precompute or set_table first");
+  try {
+    DeviceGuard g(ctx->device);
+    hipStream_t s = (hipStream_t)stream;
+    const size_t n = WB_DISPATCH(ctx, npoints());
+    const uint8_t *d = scalars;
+    if (!on_device && n) {
+      ctx->scalars.ensure(n * stride + 16);
+      MSM_HIP_CHECK(hipMemcpyAsync(ctx->scalars.p, scalars, n * stride, hipMemcpyHostToDevice, s));
+      d = ctx->scalars.as<uint8_t>();
+    }
+    if (ctx->group == 1) {
+      hfp::Jac<hfp::Fp> out;
+      ctx->g1->run(s, d, stride, (int)nbits, &out);
+      memcpy(ret, &out, sizeof out);
+    } else {
+      hfp::Jac<hfp::Fp2> out;
+      ctx->g2->run(s, d, stride, (int)nbits, &out);
+      memcpy(ret, &out, sizeof out);
+    }
+    return MSM_OK;
+  } catch (const std::exception &e) {
+    return fail(MSM_E_HIP, e.what());
+  }
+}
+
+size_t msm_wbits_ctx_table_rows(const msm_wbits_ctx *ctx) { return ctx ? WB_DISPATCH(ctx, table_rows()) : 0; }
+
+void msm_wbits_ctx_destroy(msm_wbits_ctx *ctx) { delete ctx; }
+#undef WB_DISPATCH
 
 }  // extern "C"
 

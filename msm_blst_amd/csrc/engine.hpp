@@ -315,6 +315,33 @@ class Bgmw {
   void plan_buckets(size_t n);
 };
 
+// blst's fixed-window MSM with a precomputed table of multiples (wbits.hip;
+// ref multi_scalar.c:63-261): table row i = (k+1) P_i for k < 2^(wbits-1),
+// resident in HBM; run() sums the Booth-digit gathers per window on the GPU and
+// combines the window totals on the host.
+template <int G>
+class Wbits {
+ public:
+  typedef typename HostField<G>::F HF;
+  Wbits(int device, int wbits);
+  // base points (blst affine, host or device) -> table built on the GPU
+  void precompute(const void *points_blst, size_t n, bool on_device, hipStream_t s);
+  // a table in the reference layout (blst affine, n << (wbits-1) rows), host or device
+  void set_table(const void *table_blst, size_t n, bool on_device, hipStream_t s);
+  void get_table(void *out_blst, size_t first, size_t count, hipStream_t s);
+  // scalars: n little-endian strings of `stride` bytes on device; low nbits bits used
+  void run(hipStream_t s, const uint8_t *d_scalars, size_t stride, int nbits, hfp::Jac<HF> *out);
+  size_t npoints() const { return n_; }
+  size_t table_rows() const { return n_ << (wbits_ - 1); }
+  int wbits() const { return wbits_; }
+  int device() const { return dev_; }
+
+ private:
+  int dev_, wbits_;
+  size_t n_ = 0;
+  DevBuf table_, parts_[2], fin_;
+};
+
 // blst-level tile entry points (compat.hip): sum_b weights[b] * (sum of the
 // entries of bucket b), entries (keys[k] = bucket or KEY_NONE, vals[k] = point
 // index | sign << 31) over npts blst affine points in host memory; bucket sums

@@ -291,3 +291,17 @@ def test_ches_driver_p2_n10(golden):
             assert of.compress(2, r) == run["pippenger"]
             of.lib().or_p2_bgmw_msm(r, TB, n, sc, qb, hb)
             assert of.compress(2, r) == run["pippenger"]
+
+
+def test_wbits_golden_equals_plain_msm(golden):
+    """The reference's fixed-window results (wbits.json) are plain MSMs of the
+    same inputs: every rand case equals the oracle's Pippenger sum (pins the
+    fixture's input convention: points 2^(i+1) G, seeded scalars masked to nbits)."""
+    import oracle_ffi as of
+    for c in golden("wbits.json")["cases"]:
+        if c["case"] != "rand" or c["n"] > 1024 or c["group"] != 1:
+            continue
+        n, nbits = c["n"], c["nbits"]
+        pts = of.fixed_points(1, n)
+        sc = of.repack(of.scalars(n, c["seed"]), n, nbits)
+        assert of.compress(1, of.msm(1, pts, sc, n, nbits, "pippenger")) == c["compressed"], c
