@@ -23,6 +23,7 @@
 #include "ches_kernels.hpp"
 #include "coop.hpp"
 #include "engine.hpp"
+#include "pair_kernels.hpp"
 
 #ifndef MSM_GROUP
 #error "define MSM_GROUP (1 or 2)"
@@ -273,9 +274,7 @@ void WeightedReducer<G>::launch_head(hipStream_t s, const void *Sbuf, int set) {
   const Xyzz<F> *src = reinterpret_cast<const Xyzz<F> *>(Sbuf);
   Xyzz<F> *dst = L == 1 ? dense_buf_[set].as<Xyzz<F>>() : part_[set][0].as<Xyzz<F>>();
   const uint32_t *ix = L == 1 ? idx_.as<uint32_t>() + final_perm_off_ : idx_.as<uint32_t>();
-  if (nout_[0])
-    hipLaunchKernelGGL(k_segsum<G>, dim3(nblk(nout_[0], 64)), dim3(64), 0, s, src, ix, starts_[0].as<uint32_t>(), dst,
-                       nout_[0]);
+  launch_segsum<G>(s, src, ix, starts_[0].as<uint32_t>(), dst, nout_[0]);
   MSM_HIP_CHECK(hipGetLastError());
 }
 
@@ -288,13 +287,13 @@ void WeightedReducer<G>::launch_tail(hipStream_t s, int set, bool coop) {
     const bool last = l + 1 == L;
     Xyzz<F> *dst = last ? dense_buf_[set].as<Xyzz<F>>() : part_[set][l & 1].as<Xyzz<F>>();
     const uint32_t *ix = last ? idx_.as<uint32_t>() + final_perm_off_ : nullptr;
-    if (nout_[l])
-      if (coop && nout_[l] <= 16384)  // few outputs: latency-bound, 4 waves per add
+    if (nout_[l]) {
+      if (G == 1 && coop && nout_[l] <= 16384)  // few outputs: latency-bound, 4 waves per add
         hipLaunchKernelGGL(k_segsum_c<G>, dim3(nblk(nout_[l], 64)), dim3(256), 0, s, src, ix,
                            starts_[l].as<uint32_t>(), dst, nout_[l]);
-      else
-        hipLaunchKernelGGL(k_segsum<G>, dim3(nblk(nout_[l], 64)), dim3(64), 0, s, src, ix, starts_[l].as<uint32_t>(),
-                           dst, nout_[l]);
+      else  // G2: lane pairs (fp2l.hpp) at every level
+        launch_segsum<G>(s, src, ix, starts_[l].as<uint32_t>(), dst, nout_[l]);
+    }
     MSM_HIP_CHECK(hipGetLastError());
     src = dst;
   }
@@ -503,9 +502,8 @@ void Ches<G>::accumulate(hipStream_t s, int set, int bset) {
   const size_t NB = bucket_count();
   ChesFrontSet &f = fs_[set];
   buckets_[bset].ensure(NB * sizeof(Xyzz<F>));
-  hipLaunchKernelGGL((k_accumulate<G, AffP<F>>), dim3(nblk(NB, 256)), dim3(256), 0, s, f.order.as<uint32_t>(),
-                     f.counts.as<uint32_t>(), f.offsets.as<uint32_t>(), f.sorted.as<uint32_t>(), table_.as<AffP<F>>(),
-                     buckets_[bset].as<Xyzz<F>>(), NB);
+  launch_accumulate<G>(s, f.order.as<uint32_t>(), f.counts.as<uint32_t>(), f.offsets.as<uint32_t>(),
+                       f.sorted.as<uint32_t>(), table_.as<AffP<F>>(), buckets_[bset].as<Xyzz<F>>(), NB);
   MSM_HIP_CHECK(hipGetLastError());
 }
 

@@ -16,6 +16,7 @@
 
 #include "ches_kernels.hpp"
 #include "engine.hpp"
+#include "pair_kernels.hpp"
 
 #ifndef MSM_GROUP
 #error "define MSM_GROUP (1 or 2)"
@@ -83,9 +84,9 @@ void entry_msm(void *ret, const void *pts_blst, size_t npts, const uint32_t *key
   S.buckets.ensure(nb * sizeof(Xyzz<F>));
   S.sort.run(s, S.keys.template as<uint32_t>(), S.vals.template as<uint32_t>(), ne, (uint32_t)nb, S.sorted.template as<uint32_t>(),
              S.counts.template as<uint32_t>(), S.offsets.template as<uint32_t>(), S.order.template as<uint32_t>());
-  hipLaunchKernelGGL((k_accumulate<G, Aff<F>>), dim3(nblk(nb, 256)), dim3(256), 0, s, S.order.template as<uint32_t>(),
-                     S.counts.template as<uint32_t>(), S.offsets.template as<uint32_t>(), S.sorted.template as<uint32_t>(), S.pts.template as<Aff<F>>(),
-                     S.buckets.template as<Xyzz<F>>(), nb);
+  launch_accumulate<G>(s, S.order.template as<uint32_t>(), S.counts.template as<uint32_t>(),
+                       S.offsets.template as<uint32_t>(), S.sorted.template as<uint32_t>(), S.pts.template as<Aff<F>>(),
+                       S.buckets.template as<Xyzz<F>>(), nb);
   MSM_HIP_CHECK(hipGetLastError());
   if (buckets_out) {
     S.bx.ensure(nb * 192 * G);

@@ -8,6 +8,7 @@
 #include "bucket_sort.hpp"
 #include "engine.hpp"
 #include "kernels.hpp"
+#include "pair_kernels.hpp"
 
 // compiled once per group (build.py: -DMSM_GROUP=1 and -DMSM_GROUP=2) so the
 // two instantiations build in parallel
@@ -148,9 +149,8 @@ void Pippenger<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, i
   sort_.run(s, keys_.as<uint32_t>(), vals_.as<uint32_t>(), ne, (uint32_t)NT, sorted_.as<uint32_t>(),
             counts_.as<uint32_t>(), offsets_.as<uint32_t>(), order_.as<uint32_t>());
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[2], s));
-  hipLaunchKernelGGL(k_accumulate<G>, dim3(nblk(NT, 256)), dim3(256), 0, s, order_.as<uint32_t>(),
-                     counts_.as<uint32_t>(), offsets_.as<uint32_t>(), sorted_.as<uint32_t>(), pts_.as<Aff<F>>(),
-                     buckets_.as<Xyzz<F>>(), NT);
+  launch_accumulate<G>(s, order_.as<uint32_t>(), counts_.as<uint32_t>(), offsets_.as<uint32_t>(),
+                       sorted_.as<uint32_t>(), pts_.as<Aff<F>>(), buckets_.as<Xyzz<F>>(), NT);
   MSM_HIP_CHECK(hipGetLastError());
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[3], s));
   if (red_W_ != W) {  // bucket (w, b-1) has weight b in window w; plan once per window layout

@@ -1,0 +1,123 @@
+// fp2l.hpp -- Fp2 arithmetic split over a PAIR of lanes (G2 bucket kernels).
+//
+// A G2 xyzz point is 4 Fp2 = 112 registers; the madd formulas keep ~12 Fp2
+// values live, so one lane per G2 bucket needs 256 VGPRs + 88 AGPRs and runs at
+// one wave per SIMD (measured 0.61 of the Fp-mul peak).  Here the
+// two components of every Fp2 value live in two neighbouring lanes (even lane:
+// c0, odd lane: c1), halving the registers per lane.  Products need the
+// partner's component, fetched with one DPP quad_perm move per limb, and every
+// lane runs the SAME instruction stream on lane-selected operands (v_cndmask),
+// so the pair never diverges:
+//   c0 = a0 b0 + a1 (8p - b1)        even lane: fp_mul2(a, b, a', 8p - b')
+//   c1 = a0 b1 + a1 b0               odd lane:  fp_mul2(a', b, a, b')
+// (the same single-reduction sums as f_mul(Fp2) in fp.hpp, so every column and
+// value bound of DESIGN 4a carries over unchanged; ' = partner component).
+// ec.hpp's xyzz formulas are generic over the field type and run unchanged on
+// Fp2L; ref no_asm.h:566-688 is the Fp2 tower they replace.
+#pragma once
+#include "fp.hpp"
+
+namespace msm {
+
+struct Fp2L {
+  Fp c;  // this lane's component: c0 on even lanes, c1 on odd lanes
+};
+
+MSM_FN bool pair_odd() { return (__lane_id() & 1) != 0; }
+// the partner lane's value (DPP quad_perm [1,0,3,2]: lanes 2k <-> 2k+1)
+MSM_FN uint32_t pair_swap(uint32_t x) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, true); }
+MSM_FN void pair_swap(Fp &r, const Fp &a) {
+#pragma unroll
+  for (int i = 0; i < NL; ++i) r.v[i] = pair_swap(a.v[i]);
+}
+MSM_FN void pair_sel(Fp &r, bool c, const Fp &a, const Fp &b) {  // r = c ? a : b
+#pragma unroll
+  for (int i = 0; i < NL; ++i) r.v[i] = c ? a.v[i] : b.v[i];
+}
+
+// a b, a lazy (< 6p, limbs < 2^30), b lazy (normalized here) -> S
+MSM_FN void f_mul(Fp2L &r, const Fp2L &a, const Fp2L &b) {
+  const bool odd = pair_odd();
+  Fp bn = b.c, pa, pb, nb, X, Z, W;
+  fp_norm(bn);
+  pair_swap(pa, a.c);
+  pair_swap(pb, bn);
+  fp_neg<8>(nb, pb);
+  pair_sel(X, odd, pa, a.c);
+  pair_sel(Z, odd, a.c, pa);
+  pair_sel(W, odd, pb, nb);
+  fp_mul2(r.c, X, bn, Z, W);
+}
+// b already normalized (class S)
+MSM_FN void f_mul_bs(Fp2L &r, const Fp2L &a, const Fp2L &b) {
+  const bool odd = pair_odd();
+  Fp pa, pb, nb, X, Z, W;
+  pair_swap(pa, a.c);
+  pair_swap(pb, b.c);
+  fp_neg<8>(nb, pb);
+  pair_sel(X, odd, pa, a.c);
+  pair_sel(Z, odd, a.c, pa);
+  pair_sel(W, odd, pb, nb);
+  Fp t;
+  fp_mul2(t, X, b.c, Z, W);
+  r.c = t;
+}
+// (a0 + a1 i)^2: c0 = (a0 + a1)(a0 + 16p - a1), c1 = a0 (2 a1), inputs < 6p
+MSM_FN void f_sqr(Fp2L &r, const Fp2L &a) {
+  const bool odd = pair_odd();
+  Fp own = a.c, par, s, d, X, Y;
+  fp_norm(own);
+  pair_swap(par, own);
+  fp_add(s, own, par);       // even: a0 + a1
+  fp_sub<16>(d, own, par);   // even: a0 + 16p - a1
+  fp_add(Y, own, own);       // odd: 2 a1 (limbs < 2^29)
+  pair_sel(X, odd, par, s);
+  pair_sel(Y, odd, Y, d);
+  fp_mul(r.c, X, Y);
+}
+MSM_FN void f_add(Fp2L &r, const Fp2L &a, const Fp2L &b) { fp_add(r.c, a.c, b.c); }
+MSM_FN void f_sub4(Fp2L &r, const Fp2L &a, const Fp2L &b) { fp_sub<4>(r.c, a.c, b.c); }
+MSM_FN void f_nred(Fp2L &a) { fp_nred(a.c); }
+MSM_FN void f_norm(Fp2L &a) { fp_norm(a.c); }
+MSM_FN void f_neg4(Fp2L &r, const Fp2L &a) { fp_neg<4>(r.c, a.c); }
+MSM_FN void f_one(Fp2L &r) {
+  if (pair_odd()) fp_zero(r.c);
+  else fp_one(r.c);
+}
+MSM_FN void f_zero(Fp2L &r) { fp_zero(r.c); }
+MSM_FN bool f_is_zero_exact(const Fp2L &a) {
+  const uint32_t z = fp_is_zero_exact(a.c) ? 1u : 0u;
+  return (z & pair_swap(z)) != 0;
+}
+MSM_FN bool f_is_zero_S(const Fp2L &a) {
+  const uint32_t z = fp_is_zero_lt2p(a.c) ? 1u : 0u;
+  return (z & pair_swap(z)) != 0;
+}
+MSM_FN void f_mul3(Fp2L &r, const Fp2L &a) { f_mul3(r.c, a.c); }
+// a b - c d (a lazy, b lazy normalized here, c, d in S), as f_mul_sub(Fp2):
+//   r0 = a0 b0 + a1 (8p - b1) + c0 (8p - d0) + c1 d1
+//   r1 = a0 b1 + a1 b0 + c0 (8p - d1) + c1 (8p - d0)
+MSM_FN void f_mul_sub(Fp2L &r, const Fp2L &a, const Fp2L &b, const Fp2L &c, const Fp2L &d) {
+  const bool odd = pair_odd();
+  Fp bn = b.c, pa, pb, pc, pd, nd, npd, o1, o3, o4, o5, o7, o8;
+  fp_norm(bn);
+  pair_swap(pa, a.c);
+  pair_swap(pb, bn);
+  pair_swap(pc, c.c);
+  pair_swap(pd, d.c);
+  fp_neg<8>(nd, d.c);
+  fp_neg<8>(npd, pd);
+  pair_sel(o1, odd, pa, a.c);
+  pair_sel(o3, odd, a.c, pa);
+  Fp npb;
+  fp_neg<8>(npb, pb);
+  pair_sel(o4, odd, pb, npb);
+  pair_sel(o5, odd, pc, c.c);
+  pair_sel(o7, odd, c.c, pc);
+  pair_sel(o8, odd, npd, pd);
+  Fp t;
+  fp_mul4(t, o1, bn, o3, o4, o5, nd, o7, o8);
+  r.c = t;
+}
+
+}  // namespace msm

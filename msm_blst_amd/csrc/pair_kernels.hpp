@@ -1,0 +1,115 @@
+// pair_kernels.hpp -- G2 bucket kernels on lane pairs (fp2l.hpp) and the
+// launchers every pipeline uses for the bucket accumulation and the level
+// segment sums: G1 keeps one lane per bucket / output; G2 runs two lanes per
+// bucket / output, one Fp2 component each (half the registers per lane, so
+// several waves per SIMD instead of one).
+#pragma once
+#include "ches_kernels.hpp"
+#include "fp2l.hpp"
+
+namespace msm {
+
+// component `comp` of an Fp2 stored at p (14 limbs, 8-B aligned: 56-B components)
+__device__ __forceinline__ void ld_comp(Fp &r, const Fp2 *p, int comp) {
+  const uint2 *s = reinterpret_cast<const uint2 *>(reinterpret_cast<const uint8_t *>(p) + comp * sizeof(Fp));
+#pragma unroll
+  for (int i = 0; i < NL / 2; ++i) {
+    uint2 v = s[i];
+    r.v[2 * i] = v.x;
+    r.v[2 * i + 1] = v.y;
+  }
+}
+__device__ __forceinline__ void st_comp(Fp2 *p, const Fp &a, int comp) {
+  uint2 *d = reinterpret_cast<uint2 *>(reinterpret_cast<uint8_t *>(p) + comp * sizeof(Fp));
+#pragma unroll
+  for (int i = 0; i < NL / 2; ++i) d[i] = make_uint2(a.v[2 * i], a.v[2 * i + 1]);
+}
+template <class PT>
+__device__ __forceinline__ void ld_point2l(Aff<Fp2L> &r, const PT *p, int comp) {
+  const Aff<Fp2> *q = reinterpret_cast<const Aff<Fp2> *>(p);
+  ld_comp(r.x.c, &q->x, comp);
+  ld_comp(r.y.c, &q->y, comp);
+}
+__device__ __forceinline__ void ld_xyzz2l(Xyzz<Fp2L> &r, const Xyzz<Fp2> *p, int comp) {
+  ld_comp(r.x.c, &p->x, comp);
+  ld_comp(r.y.c, &p->y, comp);
+  ld_comp(r.zzz.c, &p->zzz, comp);
+  ld_comp(r.zz.c, &p->zz, comp);
+}
+__device__ __forceinline__ void st_xyzz2l(Xyzz<Fp2> *p, const Xyzz<Fp2L> &a, int comp) {
+  st_comp(&p->x, a.x.c, comp);
+  st_comp(&p->y, a.y.c, comp);
+  st_comp(&p->zzz, a.zzz.c, comp);
+  st_comp(&p->zz, a.zz.c, comp);
+}
+
+// k_accumulate (kernels.hpp) for G2 with two lanes per bucket
+template <class PT>
+__global__ void __launch_bounds__(256) k_accumulate2p(const uint32_t *__restrict__ order,
+                                                      const uint32_t *__restrict__ counts,
+                                                      const uint32_t *__restrict__ offsets,
+                                                      const uint32_t *__restrict__ sorted, const PT *__restrict__ pts,
+                                                      Xyzz<Fp2> *__restrict__ buckets, size_t nbuckets) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 2 * nbuckets) return;  // whole pairs only: 2 nbuckets lanes
+  const int comp = (int)(t & 1);
+  const uint32_t id = order[t >> 1];
+  const uint32_t cnt = counts[id], off = offsets[id];
+  Xyzz<Fp2L> acc;
+  xyzz_set_inf(acc);
+  for (uint32_t k = 0; k < cnt; ++k) {
+    const uint32_t e = sorted[off + k];
+    Aff<Fp2L> p;
+    ld_point2l(p, &pts[e & 0x7fffffffu], comp);
+    if (f_is_zero_exact(p.x) && f_is_zero_exact(p.y)) continue;  // affine infinity (ec_ops.h:717)
+    xyzz_madd(acc, p, (e >> 31) != 0);
+  }
+  st_xyzz2l(&buckets[id], acc, comp);
+}
+
+// k_segsum (ches_kernels.hpp) for G2 with two lanes per output
+static __global__ void __launch_bounds__(256)
+    k_segsum2p(const Xyzz<Fp2> *__restrict__ src, const uint32_t *__restrict__ idx, const uint32_t *__restrict__ starts,
+               Xyzz<Fp2> *__restrict__ dst, size_t nout) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 2 * nout) return;
+  const int comp = (int)(t & 1);
+  const size_t o = t >> 1;
+  const uint32_t lo = starts[o], hi = starts[o + 1];
+  Xyzz<Fp2L> acc;
+  if (lo == hi) {
+    xyzz_set_inf(acc);
+  } else {
+    ld_xyzz2l(acc, &src[idx ? idx[lo] : lo], comp);
+    for (uint32_t k = lo + 1; k < hi; ++k) {
+      Xyzz<Fp2L> a;
+      ld_xyzz2l(a, &src[idx ? idx[k] : k], comp);
+      xyzz_add(acc, a);
+    }
+  }
+  st_xyzz2l(&dst[o], acc, comp);
+}
+
+// ---- launchers (host) ----
+template <int G, class PT>
+inline void launch_accumulate(hipStream_t s, const uint32_t *order, const uint32_t *counts, const uint32_t *offsets,
+                              const uint32_t *sorted, const PT *pts, Xyzz<typename FieldOf<G>::F> *buckets, size_t nb) {
+  if (!nb) return;
+  if constexpr (G == 1)
+    hipLaunchKernelGGL((k_accumulate<G, PT>), dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, order, counts, offsets, sorted, pts,
+                       buckets, nb);
+  else
+    hipLaunchKernelGGL((k_accumulate2p<PT>), dim3((unsigned)((2 * nb + 255) / 256)), dim3(256), 0, s, order, counts, offsets, sorted,
+                       pts, buckets, nb);
+}
+template <int G>
+inline void launch_segsum(hipStream_t s, const Xyzz<typename FieldOf<G>::F> *src, const uint32_t *idx,
+                          const uint32_t *starts, Xyzz<typename FieldOf<G>::F> *dst, size_t nout) {
+  if (!nout) return;
+  if constexpr (G == 1)
+    hipLaunchKernelGGL(k_segsum<G>, dim3((unsigned)((nout + 63) / 64)), dim3(64), 0, s, src, idx, starts, dst, nout);
+  else
+    hipLaunchKernelGGL(k_segsum2p, dim3((unsigned)((2 * nout + 63) / 64)), dim3(64), 0, s, src, idx, starts, dst, nout);
+}
+
+}  // namespace msm
