@@ -90,6 +90,36 @@ static __global__ void __launch_bounds__(256)
   st_xyzz2l(&dst[o], acc, comp);
 }
 
+// k_suffix_step / k_pair_step (ches_kernels.hpp) for G2 with two lanes per output
+static __global__ void __launch_bounds__(64)
+    k_suffix_step2p(const Xyzz<Fp2> *__restrict__ in, Xyzz<Fp2> *__restrict__ out, int S, int d, int W) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 2 * (size_t)W * S) return;
+  const int comp = (int)(t & 1);
+  const size_t o = t >> 1;
+  const int k = (int)(o % (size_t)S);
+  Xyzz<Fp2L> a;
+  ld_xyzz2l(a, &in[o], comp);
+  if (k + d < S) {
+    Xyzz<Fp2L> b;
+    ld_xyzz2l(b, &in[o + d], comp);
+    xyzz_add(a, b);
+  }
+  st_xyzz2l(&out[o], a, comp);
+}
+static __global__ void __launch_bounds__(64)
+    k_pair_step2p(const Xyzz<Fp2> *__restrict__ in, Xyzz<Fp2> *__restrict__ out, size_t nout) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 2 * nout) return;
+  const int comp = (int)(t & 1);
+  const size_t o = t >> 1;
+  Xyzz<Fp2L> a, b;
+  ld_xyzz2l(a, &in[2 * o], comp);
+  ld_xyzz2l(b, &in[2 * o + 1], comp);
+  xyzz_add(a, b);
+  st_xyzz2l(&out[o], a, comp);
+}
+
 // ---- launchers (host) ----
 template <int G, class PT>
 inline void launch_accumulate(hipStream_t s, const uint32_t *order, const uint32_t *counts, const uint32_t *offsets,
