@@ -11,9 +11,12 @@
  * Threading: entry points are thread-safe per call (each call uses its own
  * device buffers; engine contexts are not shared across threads unless the
  * caller serialises).  Errors: the blst-named functions keep blst's void
- * signatures; on a HIP failure they print the error and abort (a silent wrong
- * answer is never returned).  The msm_* extension API returns MSM_OK or a
- * negative MSM_E* code and msm_last_error() describes it.
+ * signatures; by default a HIP failure inside one prints the error and aborts
+ * (a silent wrong answer is never returned); after msm_set_abort_on_error(0)
+ * such a call returns with its result set to the all-zero point (infinity),
+ * msm_error_pending() nonzero and the message in msm_last_error().  The msm_*
+ * extension API returns MSM_OK or a negative MSM_E* code and msm_last_error()
+ * describes it.
  */
 #ifndef MSM_MI355X_H
 #define MSM_MI355X_H
@@ -181,6 +184,11 @@ enum {
 };
 typedef struct msm_ctx msm_ctx;
 const char *msm_last_error(void);
+/* void blst-named entry points on failure: 1 = print + abort (default), 0 = return
+ * with the all-zero result and raise msm_error_pending(); returns the previous mode */
+int msm_set_abort_on_error(int on);
+/* nonzero if a blst-named call of this thread failed since the last query (clears it) */
+int msm_error_pending(void);
 int msm_device_count(void);
 /* group 1 (G1) or 2 (G2); points in blst affine layout, host or device memory */
 int msm_ctx_create(msm_ctx **ctx, int group, int device, int window_bits);

@@ -81,6 +81,8 @@ def lib():
         f.argtypes, f.restype = [vp, sz, vp, sz], None
         f = getattr(L, f"blst_p{g}s_mult_wbits")
         f.argtypes, f.restype = [vp, vp, sz, sz, vp, sz, vp], None
+    L.msm_set_abort_on_error.argtypes = [i32]
+    L.msm_error_pending.argtypes = []
     L.msm_wbits_ctx_create.argtypes = [pp, i32, i32, i32]
     L.msm_wbits_ctx_precompute.argtypes = [vp, vp, sz, i32, vp]
     L.msm_wbits_ctx_set_table.argtypes = [vp, vp, sz, i32, vp]

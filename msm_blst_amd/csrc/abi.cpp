@@ -10,6 +10,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -40,10 +41,21 @@ int auto_window(size_t n) {
   return c;
 }
 
-[[noreturn]] void die(const char *where, const std::exception &e) {
-  fprintf(stderr, "msm_mi355x: %s failed: %s\n", where, e.what());
-  fflush(stderr);
-  abort();
+// Failure inside a void blst-named entry point.  Default: print and abort (a
+// wrong answer is never returned silently).  With msm_set_abort_on_error(0) the
+// call instead returns with `ret` set to the all-zero point (infinity), the
+// message in msm_last_error() and msm_error_pending() raised for the caller.
+std::atomic<int> g_abort_on_error{1};
+thread_local int g_pending = 0;
+void die(const char *where, const std::exception &e, void *ret = nullptr, size_t ret_bytes = 0) {
+  if (g_abort_on_error.load()) {
+    fprintf(stderr, "msm_mi355x: %s failed: %s\n", where, e.what());
+    fflush(stderr);
+    abort();
+  }
+  g_err = std::string(where) + " failed: " + e.what();
+  g_pending = 1;
+  if (ret) memset(ret, 0, ret_bytes);
 }
 
 template <int G>
@@ -457,7 +469,7 @@ void blst_p1s_mult_pippenger(blst_p1 *ret, const blst_p1_affine *const points[],
   try {
     mult_pippenger<1>(ret, (const void *const *)points, npoints, scalars, nbits);
   } catch (const std::exception &e) {
-    die("blst_p1s_mult_pippenger", e);
+    die("blst_p1s_mult_pippenger", e, ret, sizeof(*ret));
   }
 }
 void blst_p2s_mult_pippenger(blst_p2 *ret, const blst_p2_affine *const points[], size_t npoints,
@@ -466,7 +478,7 @@ void blst_p2s_mult_pippenger(blst_p2 *ret, const blst_p2_affine *const points[],
   try {
     mult_pippenger<2>(ret, (const void *const *)points, npoints, scalars, nbits);
   } catch (const std::exception &e) {
-    die("blst_p2s_mult_pippenger", e);
+    die("blst_p2s_mult_pippenger", e, ret, sizeof(*ret));
   }
 }
 void blst_p1s_tile_pippenger(blst_p1 *ret, const blst_p1_affine *const points[], size_t npoints,
@@ -475,7 +487,7 @@ void blst_p1s_tile_pippenger(blst_p1 *ret, const blst_p1_affine *const points[],
   try {
     tile_pippenger<1>(ret, (const void *const *)points, npoints, scalars, nbits, bit0, window);
   } catch (const std::exception &e) {
-    die("blst_p1s_tile_pippenger", e);
+    die("blst_p1s_tile_pippenger", e, ret, sizeof(*ret));
   }
 }
 void blst_p2s_tile_pippenger(blst_p2 *ret, const blst_p2_affine *const points[], size_t npoints,
@@ -484,7 +496,7 @@ void blst_p2s_tile_pippenger(blst_p2 *ret, const blst_p2_affine *const points[],
   try {
     tile_pippenger<2>(ret, (const void *const *)points, npoints, scalars, nbits, bit0, window);
   } catch (const std::exception &e) {
-    die("blst_p2s_tile_pippenger", e);
+    die("blst_p2s_tile_pippenger", e, ret, sizeof(*ret));
   }
 }
 
@@ -531,7 +543,7 @@ MSM_XYZZ_HELPERS(2, hfp::Fp2)
       for (size_t k = 0; k < bucket_set_size; ++k) w[k] = (uint32_t)std::max(bucket_set_ascend[k], 0);           \
       weighted_bucket_sum<g>(out, buckets, bucket_set_size, w.data());                                            \
     } catch (const std::exception &e) {                                                                           \
-      die("blst_p" #g "_integrate_buckets_accumulation_d_CHES", e);                                               \
+      die("blst_p" #g "_integrate_buckets_accumulation_d_CHES", e, out, sizeof(*out));                                               \
     }                                                                                                             \
   }                                                                                                               \
   void blst_p##g##_construct_nh_scalars_nh_points(int nh_scalars[], unsigned char booth_signs[],                  \
@@ -554,7 +566,7 @@ MSM_XYZZ_HELPERS(2, hfp::Fp2)
       tile_d_ches<g>(ret, (const void *const *)points, npoints, scalars, booth_signs, buckets, bucket_set_ascend, \
                      bucket_value_to_its_index, bucket_set_size);                                                 \
     } catch (const std::exception &e) {                                                                           \
-      die("blst_p" #g "_tile_pippenger_d_CHES", e);                                                               \
+      die("blst_p" #g "_tile_pippenger_d_CHES", e, ret, sizeof(*ret));                                                               \
     }                                                                                                             \
   }                                                                                                               \
   void blst_p##g##_tile_pippenger_d_CHES_noindexhash(                                                             \
@@ -566,7 +578,7 @@ MSM_XYZZ_HELPERS(2, hfp::Fp2)
       tile_d_ches_noindex<g>(ret, (const void *const *)points, npoints, scalars, booth_signs, buckets,            \
                              bucket_set_ascend, bucket_set_size);                                                 \
     } catch (const std::exception &e) {                                                                           \
-      die("blst_p" #g "_tile_pippenger_d_CHES_noindexhash", e);                                                   \
+      die("blst_p" #g "_tile_pippenger_d_CHES_noindexhash", e, ret, sizeof(*ret));                                                   \
     }                                                                                                             \
   }                                                                                                               \
   void blst_p##g##_tile_pippenger_CHES_prefetch_2step_ahead_input_std_scalar(                                     \
@@ -578,7 +590,7 @@ MSM_XYZZ_HELPERS(2, hfp::Fp2)
       tile_ches_std<g>(ret, table, npoints, scalars, H, buckets, bucket_set_ascend, bucket_value_to_its_index,    \
                        bucket_set_size);                                                                          \
     } catch (const std::exception &e) {                                                                           \
-      die("blst_p" #g "_tile_pippenger_CHES_prefetch_2step_ahead_input_std_scalar", e);                           \
+      die("blst_p" #g "_tile_pippenger_CHES_prefetch_2step_ahead_input_std_scalar", e, ret, sizeof(*ret));                           \
     }                                                                                                             \
   }                                                                                                               \
   void blst_p##g##_tile_pippenger_BGMW95(blst_p##g *ret, const blst_p##g##_affine *const points[], size_t npoints, \
@@ -587,7 +599,7 @@ MSM_XYZZ_HELPERS(2, hfp::Fp2)
     try {                                                                                                         \
       tile_bgmw95<g>(ret, (const void *const *)points, npoints, scalars, booth_signs, buckets, q_exponent);       \
     } catch (const std::exception &e) {                                                                           \
-      die("blst_p" #g "_tile_pippenger_BGMW95", e);                                                               \
+      die("blst_p" #g "_tile_pippenger_BGMW95", e, ret, sizeof(*ret));                                                               \
     }                                                                                                             \
   }
 MSM_CHES_ENTRIES(1)
@@ -602,7 +614,7 @@ MSM_CHES_ENTRIES(2)
     try {                                                                                                         \
       points_add<g>(ret, (const void *const *)points, npoints);                                                   \
     } catch (const std::exception &e) {                                                                           \
-      die("blst_p" #g "s_add", e);                                                                                \
+      die("blst_p" #g "s_add", e, ret, sizeof(*ret));                                                                                \
     }                                                                                                             \
   }
 MSM_POINTS_ADD(1)
@@ -631,7 +643,7 @@ MSM_POINTS_ADD(2)
     try {                                                                                                         \
       wbits_mult<g>(ret, table, wbits, npoints, scalars, nbits);                                                  \
     } catch (const std::exception &e) {                                                                           \
-      die("blst_p" #g "s_mult_wbits", e);                                                                         \
+      die("blst_p" #g "s_mult_wbits", e, ret, sizeof(*ret));                                                                         \
     }                                                                                                             \
   }
 MSM_WBITS_ENTRIES(1, 8192)  /* SCRATCH_SZ of ref multi_scalar.c:78 */
@@ -639,6 +651,14 @@ MSM_WBITS_ENTRIES(2, 4096)
 #undef MSM_WBITS_ENTRIES
 
 const char *msm_last_error(void) { return g_err.c_str(); }
+
+int msm_set_abort_on_error(int on) { return g_abort_on_error.exchange(on != 0 ? 1 : 0); }
+
+int msm_error_pending(void) {
+  const int p = g_pending;
+  g_pending = 0;
+  return p;
+}
 
 int msm_device_count(void) {
   int n = 0;

@@ -52,3 +52,13 @@ def test_library_loads_and_scratch_sizeof_matches_blst(built):
     # sizeof(blst_p1xyzz) << (window(n)-1), window rule of multi_scalar.c:268-275
     for n, w in ((1024, 8), (65536, 13), (1 << 20, 17), (1 << 21, 18), (16, 2), (2, 2), (1, 1)):
         assert L.blst_p1s_mult_pippenger_scratch_sizeof(n) == 192 << (w - 1)
+
+
+def test_error_mode_switch(built):
+    """msm_set_abort_on_error toggles the void entry points' failure mode and
+    returns the previous one (default: abort); nothing is pending initially."""
+    L = ctypes.CDLL(built)
+    L.msm_set_abort_on_error.argtypes = [ctypes.c_int]
+    assert L.msm_set_abort_on_error(0) == 1
+    assert L.msm_set_abort_on_error(1) == 0
+    assert L.msm_error_pending() == 0

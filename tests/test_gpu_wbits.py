@@ -92,3 +92,26 @@ def test_wbits_in_place_precompute_and_pointer_rules(m, golden):
     assert L.blst_p1s_mult_wbits_scratch_sizeof(100) == 144 * 100
     assert L.blst_p1s_mult_wbits_scratch_sizeof(1 << 20) == 144 * 8192
     assert L.blst_p2s_mult_wbits_scratch_sizeof(1 << 20) == 288 * 4096
+
+
+def test_error_mode_returns_infinity_instead_of_abort(m):
+    """With msm_set_abort_on_error(0) a failing void entry point (wbits = 15 is
+    outside blst's [2, 14]) returns the all-zero point and raises
+    msm_error_pending() instead of aborting the process."""
+    L = m.lib()
+    prev = L.msm_set_abort_on_error(0)
+    try:
+        n = 4
+        pts = bytes(m.fixed_points(1, n))
+        table = (ctypes.c_uint8 * (96 * n * 2))()
+        sc = bytes(m.gen_scalars(n, 1))
+        ret = (ctypes.c_uint8 * 144)(*([0xAB] * 144))
+        S = (ctypes.c_uint8 * len(sc)).from_buffer_copy(sc)
+        sp = (ctypes.c_void_p * 2)(ctypes.cast(S, ctypes.c_void_p), None)
+        L.blst_p1s_mult_wbits(ret, table, 15, n, sp, 255, None)
+        assert bytes(ret) == bytes(144)
+        assert L.msm_error_pending() == 1
+        assert L.msm_error_pending() == 0
+        assert b"wbits" in L.msm_last_error()
+    finally:
+        L.msm_set_abort_on_error(prev)
