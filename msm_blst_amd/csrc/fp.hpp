@@ -322,7 +322,7 @@ MSM_FN void fp_canon(Fp &r, const Fp &a) {
 
 // Reduce a normalized value v < 32p to [0, 2p) (class S): quotient estimate
 // from the top limb, q = floor(v13 * floor(2^32/(p13+1)) / 2^32) <= floor(v/p);
-// v - q*p < 1.0003p (verified exhaustively over the top limb in DESIGN.md).
+// v - q*p < 1.0003p (checked exhaustively over the top limb: tests/fp_bounds.py red()).
 constexpr uint32_t RED_MAG = 0x9d83;  // floor(2^32 / (p13 + 1)), p13 = 0x1a011
 MSM_FN void fp_red(Fp &a) {
   uint32_t q = (uint32_t)(((uint64_t)a.v[NL - 1] * RED_MAG) >> 32);

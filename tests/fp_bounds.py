@@ -237,6 +237,11 @@ def sqr_fp2(a):            # f_sqr(Fp2): both normalized, (a0+a1)(a0-a1), 2 a0 a
     return union(c0, c1)
 
 
+def sqr_fp2l(a):           # f_sqr(Fp2L, fp2l.hpp): own component normalized, partner swapped in;
+    an = norm(a)           # even lane (a0 + a1)(a0 + 16p - a1), odd lane a0 (2 a1), one fp_mul each
+    return union(mul(add(an, an), sub(an, an, 16)), mul(an, add(an, an)))
+
+
 def mul_sub_fp2(a, b, c, d):   # f_mul_sub(Fp2): two fp_mul4 with 8p-adjusted negations
     b0 = norm(b)
     nb1 = neg(b0, 8)
@@ -256,8 +261,8 @@ class Field:
     def mul_bs(self, a, b):
         return mul(a, b) if self.g == 1 else mul_bs_fp2(a, b)
 
-    def sqr(self, a):
-        return sqr(a) if self.g == 1 else sqr_fp2(a)
+    def sqr(self, a):  # group 3: G2 on lane pairs (fp2l.hpp) -- only the square differs
+        return sqr(a) if self.g == 1 else (sqr_fp2l(a) if self.g == 3 else sqr_fp2(a))
 
     def mul_sub(self, a, b, c, d):
         if self.g == 1:
@@ -379,6 +384,16 @@ def prove_all():
         res[f"G{g} xyzz_add doubling branch"] = list(dbl)
         res[f"G{g} xyzz_dbl"] = list(trace_dbl(g))
         res[f"G{g} coop_xyzz_add"] = list(trace_coop_add(g))
+    # G2 on lane pairs (fp2l.hpp): the same formulas over f_mul / f_mul_bs / f_mul_sub
+    # of the one-lane Fp2 and a square split per lane
+    for negate in (False, True):
+        main, dbl = trace_madd(3, negate)
+        res[f"G2-pairs xyzz_madd{' (neg)' if negate else ''}"] = list(main)
+        res[f"G2-pairs xyzz_madd doubling branch{' (neg)' if negate else ''}"] = list(dbl)
+    main, dbl = trace_add(3)
+    res["G2-pairs xyzz_add"] = list(main)
+    res["G2-pairs xyzz_add doubling branch"] = list(dbl)
+    res["G2-pairs xyzz_dbl"] = list(trace_dbl(3))
     for name, outs in res.items():
         for k, o in enumerate(outs):
             need(o.is_S(), f"{name}: output {'x y zzz zz'.split()[k]} not in class S: {o}")

@@ -48,7 +48,7 @@ def shim():
 
 def test_interval_model_proves_every_formula():
     res = fb.prove_all()
-    assert len(res) == 16
+    assert len(res) == 16 + 7  # G1, G2 (one lane), G2 on lane pairs
     for name, outs in res.items():
         assert all(o.is_S() for o in outs), name
 
