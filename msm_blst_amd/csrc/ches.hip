@@ -307,6 +307,51 @@ void WeightedReducer<G>::launch_tail(hipStream_t s, int set, bool coop) {
 }
 
 template <int G>
+void WeightedReducer<G>::ensure_group(int set, int nmsm) {
+  typedef typename FieldOf<G>::F F;
+  if (set < 0 || set >= NSETS || nmsm < 1) throw std::runtime_error("WeightedReducer: bad group");
+  part_[set][0].ensure((size_t)nmsm * maxp_ * sizeof(Xyzz<F>));
+  part_[set][1].ensure((size_t)nmsm * maxp_ * sizeof(Xyzz<F>));
+  dense_buf_[set].ensure((size_t)nmsm * dense_slots() * sizeof(Xyzz<F>));
+  const size_t NT = (size_t)nmsm * dense_slots();  // ScanReducer::launch's buffers for W = 2 nwin nmsm
+  dense_[set].buf[0].ensure(NT * sizeof(Xyzz<F>));
+  dense_[set].buf[1].ensure(NT * sizeof(Xyzz<F>));
+  dense_[set].fin.ensure((size_t)nmsm * out_bytes());
+}
+
+template <int G>
+void WeightedReducer<G>::launch_head_slot(hipStream_t s, const void *Sbuf, int set, int slot) {
+  typedef typename FieldOf<G>::F F;
+  const bool only = nout_.size() == 1;  // level 0 is also the last level
+  Xyzz<F> *dst = only ? dense_buf_[set].as<Xyzz<F>>() + (size_t)slot * dense_slots()
+                      : part_[set][0].as<Xyzz<F>>() + (size_t)slot * maxp_;
+  const uint32_t *ix = only ? idx_.as<uint32_t>() + final_perm_off_ : idx_.as<uint32_t>();
+  launch_segsum<G>(s, reinterpret_cast<const Xyzz<F> *>(Sbuf), ix, starts_[0].as<uint32_t>(), dst, nout_[0]);
+  MSM_HIP_CHECK(hipGetLastError());
+}
+
+template <int G>
+void WeightedReducer<G>::launch_tail_group(hipStream_t s, int set, int nmsm) {
+  typedef typename FieldOf<G>::F F;
+  const size_t L = nout_.size();
+  const Xyzz<F> *src = part_[set][0].as<Xyzz<F>>();
+  for (size_t l = 1; l < L; ++l) {
+    const bool last = l + 1 == L;
+    Xyzz<F> *dst = last ? dense_buf_[set].as<Xyzz<F>>() : part_[set][l & 1].as<Xyzz<F>>();
+    const uint32_t *ix = last ? idx_.as<uint32_t>() + final_perm_off_ : nullptr;
+    launch_segsum<G>(s, src, ix, starts_[l].as<uint32_t>(), dst, nout_[l], nmsm, maxp_, last ? dense_slots() : maxp_);
+    MSM_HIP_CHECK(hipGetLastError());
+    src = dst;
+  }
+  dense_[set].launch(s, dense_buf_[set].p, 2 * nwin_ * nmsm, 1 << sbits_, false);
+}
+
+template <int G>
+void WeightedReducer<G>::copy_out_group(hipStream_t s, int set, int nmsm, void *host) {
+  MSM_HIP_CHECK(hipMemcpyAsync(host, dense_[set].fin.p, (size_t)nmsm * out_bytes(), hipMemcpyDeviceToHost, s));
+}
+
+template <int G>
 void WeightedReducer<G>::copy_out(hipStream_t s, int set, void *host) {
   MSM_HIP_CHECK(hipMemcpyAsync(host, dense_[set].fin.p, out_bytes(), hipMemcpyDeviceToHost, s));
 }
@@ -575,7 +620,10 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
   }
   // one pinned read-back slot per MSM of the batch: the host never waits inside
   // the issue loop, so MSM k+1's front is queued while MSM k still accumulates
-  const size_t ob = (red_.out_bytes() + 255) & ~(size_t)255;
+  const size_t ob = red_.out_bytes();  // a group's read-back lands contiguously
+  // reduction groups of R <= kGroup MSMs (balanced sizes), alternating between
+  // the two reducer sets / tail streams
+  const size_t ngroups = (count + kGroup - 1) / kGroup, R = (count + ngroups - 1) / ngroups;
   if (host_out_bytes_ < count * ob) {
     if (host_out_) (void)hipHostFree(host_out_);
     host_out_ = nullptr;
@@ -586,10 +634,8 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
   // every buffer the loop touches exists before the first launch (an allocation
   // inside the issue loop could synchronise the device)
   const size_t NB = bucket_count(), n = n_;
-  for (int b = 0; b < kBSets && (size_t)b < count; ++b) {
-    buckets_[b].ensure(NB * sizeof(Xyzz<typename FieldOf<G>::F>));
-    red_.ensure_set(b);
-  }
+  for (int b = 0; b < kBSets && (size_t)b < count; ++b) buckets_[b].ensure(NB * sizeof(Xyzz<typename FieldOf<G>::F>));
+  for (int t = 0; t < kBSets && (size_t)t < ngroups; ++t) red_.ensure_group(t, (int)R);
   if (scalars_on_host)
     for (int f = 0; f < kSlots && (size_t)f < count; ++f) scal_[f].ensure(n * stride + 16);
   const bool prof = profile_;
@@ -611,15 +657,23 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
   //   s:         accumulation k into bucket set k % kBSets (after MSM k-2's
   //              reduction head released it) -- back to back, the VALU-bound
   //              critical path;
-  //   tails_[t]: the whole reduction of MSM k, t = k % kBSets (level 0,
-  //              latency-bound tail, read-back) beside the next accumulations --
-  //              two streams, so MSM k+1's level 0 never queues behind MSM k's
-  //              latency-bound tail (one shared stream: 352 vs 412 M pairs/s);
+  //   tails_[t]: the reductions of group g = k / R, t = g % 2: level 0 of each
+  //              MSM into its slot of reducer set t right after its accumulation,
+  //              then, after the group's last MSM, ONE launch per tail level for
+  //              the whole group and one read-back.  Every launch that runs
+  //              beside an accumulation costs it ~10-20 us (profiles/
+  //              r02_batch_sched2.txt: skipping the per-MSM tail levels sped the
+  //              batch from 2.52 to 2.25 ms per MSM), so the ~35 latency-bound
+  //              levels are paid once per group, not once per MSM (groups of 8:
+  //              2.47 -> 2.35 ms per MSM; 4 and 20 measure the same).  Two streams:
+  //              group g+1's level 0s never queue behind group g's tail;
   //   cstream_:  host scalars: the H2D copy of set k + kSlots into the slot front
   //              k has consumed, on its own stream (copies on the front stream:
   //              -5 %, on the reduction streams: -15 %; own stream: -2 % vs
   //              resident scalars).
   // No host waits inside the loop: every MSM has its own pinned read-back slot.
+  // Reducer set t is reused by group g + 2 only after group g's tail: both are
+  // in order on tails_[t].
   while (bev_.size() < 4 * count + 1) {
     hipEvent_t e;
     MSM_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -638,7 +692,8 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
   for (size_t k = 0; k < (size_t)kSlots; ++k) copy_set(k);
   for (size_t k = 0; k < count; ++k) {
     const int bset = (int)(k % kBSets), fset = (int)(k % kFronts);
-    hipStream_t ts = tails_[bset];
+    const int slot = (int)(k % R), gset = (int)((k / R) % 2);
+    hipStream_t ts = tails_[gset];
     const uint8_t *src = scalars + k * set_stride;
     if (scalars_on_host) {
       src = scal_[k % kSlots].as<uint8_t>();
@@ -658,10 +713,12 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
     if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k + 1], s));
     MSM_HIP_CHECK(hipEventRecord(eva[k], s));
     MSM_HIP_CHECK(hipStreamWaitEvent(ts, eva[k], 0));
-    red_.launch_head(ts, buckets_[bset].p, bset);
+    red_.launch_head_slot(ts, buckets_[bset].p, gset, slot);
     MSM_HIP_CHECK(hipEventRecord(evh[k], ts));
-    red_.launch_tail(ts, bset, false);  // beside the accumulations: least resource time
-    red_.copy_out(ts, bset, (uint8_t *)host_out_ + k * ob);
+    if ((size_t)slot + 1 == R || k + 1 == count) {  // the group's last MSM
+      red_.launch_tail_group(ts, gset, slot + 1);
+      red_.copy_out_group(ts, gset, slot + 1, (uint8_t *)host_out_ + (k - slot) * ob);
+    }
   }
   // the caller's stream observes completion of every reduction (and front)
   for (int t = 0; t < kBSets; ++t) {

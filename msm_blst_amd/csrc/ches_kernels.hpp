@@ -372,13 +372,18 @@ static __global__ void __launch_bounds__(256)
 
 // ------------------------------------------------------------ segment sums --
 // dst[t] = sum_{k in [starts[t], starts[t+1])} src[idx ? idx[k] : k]   (xyzz)
+// for each of gridDim.y MSMs of a batch group: MSM blockIdx.y reads src +
+// y src_stride and writes dst + y dst_stride (the same plan for every MSM)
 template <int G>
 static __global__ void __launch_bounds__(256)
     k_segsum(const Xyzz<typename FieldOf<G>::F> *__restrict__ src, const uint32_t *__restrict__ idx,
-             const uint32_t *__restrict__ starts, Xyzz<typename FieldOf<G>::F> *__restrict__ dst, size_t nout) {
+             const uint32_t *__restrict__ starts, Xyzz<typename FieldOf<G>::F> *__restrict__ dst, size_t nout,
+             size_t src_stride, size_t dst_stride) {
   typedef typename FieldOf<G>::F F;
   size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= nout) return;
+  src += blockIdx.y * src_stride;
+  dst += blockIdx.y * dst_stride;
   uint32_t lo = starts[t], hi = starts[t + 1];
   Xyzz<F> acc;
   if (lo == hi) {

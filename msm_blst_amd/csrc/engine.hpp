@@ -163,7 +163,18 @@ class WeightedReducer {
 
   void ensure_set(int set);  // allocate buffer set `set` for the current plan
 
+  // Batch groups (Ches::run_batch): the reduction plan is the same for every
+  // MSM, so nmsm MSMs share buffer set `set` -- each MSM's level 0 writes its
+  // own slot, then ONE launch per tail level reduces all slots together.  A
+  // batch then issues ~35 tail launches per group instead of per MSM (every
+  // launch beside an accumulation costs it time).
+  void ensure_group(int set, int nmsm);
+  void launch_head_slot(hipStream_t s, const void *S, int set, int slot);
+  void launch_tail_group(hipStream_t s, int set, int nmsm);          // levels >= 1, dense, finalize
+  void copy_out_group(hipStream_t s, int set, int nmsm, void *host);  // nmsm * out_bytes()
+
  private:
+  size_t dense_slots() const { return (size_t)2 * nwin_ << sbits_; }
   size_t bsize_ = 0, final_perm_off_ = 0, maxp_ = 1;
   int sbits_ = 1, nwin_ = 1;
   DevBuf idx_, dense_buf_[NSETS], part_[NSETS][2];
@@ -259,6 +270,7 @@ class Ches {
   DevBuf code_, rank_, table_, buckets_[kBSets];
   // digit/sort outputs, one set per in-flight front so that MSM k+1's digits
   // and sort (memory/LDS-bound) run beside MSM k's accumulation (VALU-bound)
+  static constexpr int kGroup = 8;   // batch: MSMs per reduction group (WeightedReducer::launch_tail_group)
   static constexpr int kFronts = 3;  // batch: front k+1 runs in MSM k-1's accumulation tail
   ChesFrontSet fs_[kFronts];
   static constexpr int kSlots = 4;   // device slots of host scalar sets in a batch

@@ -70,9 +70,11 @@ __global__ void __launch_bounds__(256) k_accumulate2p(const uint32_t *__restrict
 // k_segsum (ches_kernels.hpp) for G2 with two lanes per output
 static __global__ void __launch_bounds__(256)
     k_segsum2p(const Xyzz<Fp2> *__restrict__ src, const uint32_t *__restrict__ idx, const uint32_t *__restrict__ starts,
-               Xyzz<Fp2> *__restrict__ dst, size_t nout) {
+               Xyzz<Fp2> *__restrict__ dst, size_t nout, size_t src_stride, size_t dst_stride) {
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= 2 * nout) return;
+  src += blockIdx.y * src_stride;  // MSM blockIdx.y of a batch group (k_segsum)
+  dst += blockIdx.y * dst_stride;
   const int comp = (int)(t & 1);
   const size_t o = t >> 1;
   const uint32_t lo = starts[o], hi = starts[o + 1];
@@ -132,14 +134,18 @@ inline void launch_accumulate(hipStream_t s, const uint32_t *order, const uint32
     hipLaunchKernelGGL((k_accumulate2p<PT>), dim3((unsigned)((2 * nb + 255) / 256)), dim3(256), 0, s, order, counts, offsets, sorted,
                        pts, buckets, nb);
 }
+// nmsm > 1: the same segment sums for nmsm MSMs of a batch group in one launch
 template <int G>
 inline void launch_segsum(hipStream_t s, const Xyzz<typename FieldOf<G>::F> *src, const uint32_t *idx,
-                          const uint32_t *starts, Xyzz<typename FieldOf<G>::F> *dst, size_t nout) {
-  if (!nout) return;
+                          const uint32_t *starts, Xyzz<typename FieldOf<G>::F> *dst, size_t nout, int nmsm = 1,
+                          size_t src_stride = 0, size_t dst_stride = 0) {
+  if (!nout || nmsm < 1) return;
   if constexpr (G == 1)
-    hipLaunchKernelGGL(k_segsum<G>, dim3((unsigned)((nout + 63) / 64)), dim3(64), 0, s, src, idx, starts, dst, nout);
+    hipLaunchKernelGGL(k_segsum<G>, dim3((unsigned)((nout + 63) / 64), (unsigned)nmsm), dim3(64), 0, s, src, idx, starts,
+                       dst, nout, src_stride, dst_stride);
   else
-    hipLaunchKernelGGL(k_segsum2p, dim3((unsigned)((2 * nout + 63) / 64)), dim3(64), 0, s, src, idx, starts, dst, nout);
+    hipLaunchKernelGGL(k_segsum2p, dim3((unsigned)((2 * nout + 63) / 64), (unsigned)nmsm), dim3(64), 0, s, src, idx,
+                       starts, dst, nout, src_stride, dst_stride);
 }
 
 }  // namespace msm
