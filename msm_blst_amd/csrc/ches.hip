@@ -624,20 +624,23 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
   // reduction groups of R <= kGroup MSMs (balanced sizes), alternating between
   // the two reducer sets / tail streams
   const size_t ngroups = (count + kGroup - 1) / kGroup, R = (count + ngroups - 1) / ngroups;
-  if (host_out_bytes_ < count * ob) {
+  if (host_out_bytes_ < count * ob) {  // at least 256 MSMs' worth (a few hundred KiB): no regrowth per batch size
     if (host_out_) (void)hipHostFree(host_out_);
     host_out_ = nullptr;
     host_out_bytes_ = 0;
-    MSM_HIP_CHECK(hipHostMalloc(&host_out_, count * ob, hipHostMallocDefault));
-    host_out_bytes_ = count * ob;
+    const size_t bytes = std::max<size_t>(count, 256) * ob;
+    MSM_HIP_CHECK(hipHostMalloc(&host_out_, bytes, hipHostMallocDefault));
+    host_out_bytes_ = bytes;
   }
   // every buffer the loop touches exists before the first launch (an allocation
   // inside the issue loop could synchronise the device)
   const size_t NB = bucket_count(), n = n_;
   for (int b = 0; b < kBSets && (size_t)b < count; ++b) buckets_[b].ensure(NB * sizeof(Xyzz<typename FieldOf<G>::F>));
-  for (int t = 0; t < kBSets && (size_t)t < ngroups; ++t) red_.ensure_group(t, (int)R);
+  // sized for kGroup whatever this batch's R: a later, larger batch must not
+  // reallocate (a hipFree inside the pipelined region would synchronise it)
+  for (int t = 0; t < kBSets && (size_t)t < ngroups; ++t) red_.ensure_group(t, kGroup);
   if (scalars_on_host)
-    for (int f = 0; f < kSlots && (size_t)f < count; ++f) scal_[f].ensure(n * stride + 16);
+    for (int f = 0; f < kSlots; ++f) scal_[f].ensure(n * stride + 16);
   const bool prof = profile_;
   profile_ = false;
   if (prof)

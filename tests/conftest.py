@@ -11,6 +11,20 @@ if TESTS not in sys.path:
     sys.path.insert(0, TESTS)
 
 
+@pytest.fixture(scope="session", autouse=True)
+def _torch_hip_first(request):
+    """GPU sessions: let torch initialise its HIP runtime before the engine's
+    library does.  Some tests hand torch tensors (pinned host memory, device
+    buffers) to the engine; with the engine's HIP runtime initialised first,
+    torch's own initialisation in the same process then found no device (seen
+    when a subset of the GPU tests ran without an earlier torch user)."""
+    if any(item.get_closest_marker("gpu") for item in request.session.items):
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    yield
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path through the C ABI)")
     config.addinivalue_line("markers", "slow: long-running parity case")

@@ -27,15 +27,17 @@ torch.cuda.synchronize()
 ctx.set_profiling(True)
 ref = None
 for name, ptr, ondev in (("resident", d_all.data_ptr(), True), ("h2d", host.data_ptr(), False)):
-    best = 1e9
+    best, runs = 1e9, []
     for r in range(R):
         torch.cuda.synchronize()
         t = time.perf_counter()
         parts = ctx.mult_batch(ptr, K, 32, set_stride=n * 32, on_device=ondev, stream=sp)
         torch.cuda.synchronize()
+        runs.append(n * K / (time.perf_counter() - t) / 1e6)
         best = min(best, time.perf_counter() - t)
         keys = [m.compress(1, j) for j in parts]
         ok = ref is None or keys == ref
         ref = ref or keys
     print(f"EXP {name}: {n * K / best / 1e6:.1f} M pairs/s "
-          f"({best / K * 1e3:.3f} ms/MSM, acc {ctx.phase_times()['accumulate']:.3f} ms) same={ok}", flush=True)
+          f"({best / K * 1e3:.3f} ms/MSM, acc {ctx.phase_times()['accumulate']:.3f} ms) same={ok} runs={[round(x) for x in runs]}",
+          flush=True)
