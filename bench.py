@@ -49,6 +49,7 @@ FPMUL_PEAK = 76.8e9            # measured register-resident Fp-mul/s: profiles/r
 AFFINE_BYTES = 96              # one G1 affine point (blst layout), SURVEY 8d
 FPMUL_PER_MADD = 10            # 8M + 2S (ec_ops.h:727-748)
 CPU_THREADS = 16               # the GPU box's CPU share per GPU (16 threads)
+DEFAULT_BETA = {}              # log_n -> ches_config_files variant used by default (measured on MI355X)
 
 
 def log(*a):
@@ -120,6 +121,9 @@ def main():
     ap.add_argument("--group", type=int, choices=(1, 2), default=1,
                     help="1: G1 (the BASELINE metric); 2: G2 (configs[4], Fp2 tower), reported under its own metric")
     ap.add_argument("--window", type=int, default=16, help="plain Pippenger window bits")
+    ap.add_argument("--beta", type=int, choices=(0, 1), default=None,
+                    help="CHES/BGMW95 configuration: ches_config_files/config_file_n_exp_<log_n>[_beta].h "
+                         "(default: the faster one measured on MI355X where the reference ships both)")
     ap.add_argument("--no-compare", action="store_true", help="skip the resident/sync/other-method legs")
     ap.add_argument("--no-batch", action="store_true",
                     help="CHES: time K independent synchronous MSMs instead of one pipelined batch of K")
@@ -175,13 +179,26 @@ def main():
             return parts
         return [mdist.fold(ps, add) for ps in mdist.gather_partials_batch(parts, G, xdev)]
 
-    def make(method):
+    def has_config(b):
+        try:
+            m.ches.params(args.log_n, b)
+            return True
+        except Exception:
+            return False
+
+    beta = args.beta if args.beta is not None else DEFAULT_BETA.get(args.log_n, 0)
+    if not has_config(beta):
+        log(f"no reference configuration n_exp={args.log_n} beta={beta}; using beta=0")
+        beta = 0
+
+    def make(method, b=None):
         t = time.time()
+        b = beta if b is None else b
         if method == "ches":
-            ctx = m.CHESContext(G, local, n_exp=args.log_n)
+            ctx = m.CHESContext(G, local, n_exp=args.log_n, beta=b)
             ctx.build_table(pts, n, stream=sp)
         elif method == "bgmw":
-            ctx = m.BGMWContext(G, local, n_exp=args.log_n)
+            ctx = m.BGMWContext(G, local, n_exp=args.log_n, beta=b)
             ctx.build_table(pts, n, stream=sp)
         else:
             ctx = m.MSMContext(G, local, args.window)
@@ -227,6 +244,20 @@ def main():
                                            "kernel_ms": round(ctx.phase_times()["accumulate"], 4),
                                            "equals_h2d_batch": keys(rparts) == keys(res),
                                            "note": "the same K sets already resident in HBM (kernel-only rate)"}
+            if world == 1 and has_config(1 - beta):  # the reference's other configuration for this n
+                octx, _ = make("ches", 1 - beta)
+                octx.mult_batch(dptr, min(max(W, 1), K), 32, set_stride=SS, on_device=True, stream=sp)
+                with Bracket(world, dev, xdev) as b:
+                    oparts = octx.mult_batch(dptr, K, 32, set_stride=SS, on_device=True, stream=sp)
+                op = octx.params
+                legs[f"ches_batch_resident_beta{1 - beta}"] = {
+                    "value": round(n * K / b.elapsed, 1), "ms_per_step": round(b.elapsed / K * 1e3, 4),
+                    "kernel_ms": round(octx.phase_times()["accumulate"], 4),
+                    "equals_h2d_batch": keys(oparts) == keys(res),
+                    "note": f"the reference's other n=2^{args.log_n} configuration "
+                            f"(config_file_n_exp_{args.log_n}{'_beta' if beta == 0 else ''}.h: q=2^{op['q_exp']}, "
+                            f"h={op['h']}, |B|={op['b_size']}), same K resident sets"}
+                octx.close()
             sres, sel = sync_steps(mult, K, True)
             legs["ches_sync"] = {"value": round(n * world * K / sel, 1), "ms_per_step": round(sel / K * 1e3, 4),
                                  "note": "K synchronous msm_ches_ctx_mult calls on resident sets (per-MSM latency)"}
@@ -294,7 +325,9 @@ def main():
         workload = (f"G{G} MSM n=2^{args.log_n} per GPU, CHES nh+q/5 (q=2^{ctx.params['q_exp']}, h={h}, "
                     f"|B|={ctx.params['b_size']}), table T=m*q^j*P_i resident in HBM, K distinct scalar sets "
                     f"H2D from pinned host memory inside the timed region")
-        cfg_extra = {"method": "ches_q_over_5", "q_exp": ctx.params["q_exp"], "h": h,
+        cfg_extra = {"method": "ches_q_over_5", "beta": beta,
+                     "config_file": f"ches_config_files/config_file_n_exp_{args.log_n}{'_beta' if beta else ''}.h",
+                     "q_exp": ctx.params["q_exp"], "h": h,
                      "bucket_set": ctx.params["b_size"], "buckets_incl_top_digit_copies": ctx.bucket_count()}
     elif args.method == "bgmw":
         h = ctx.h

@@ -12,7 +12,15 @@
 //   k_bs_coarse   per tile: LDS rank within (tile, bin) -> coarse-sorted keys/vals
 //   k_bs_fine     one 1024-thread workgroup per coarse bin: LDS histogram over
 //                 its 2^fb_bits buckets, block scan, counts/offsets out, vals
-//                 placed in bucket order in LDS windows and streamed out
+//                 placed in bucket order in LDS windows and streamed out; also
+//                 the accumulation schedule's class histogram
+//   k_sched_scatter  bucket ids ordered by entry count (the schedule)
+//
+// Seven launches per sort including the digit kernel that feeds it (hist,
+// two hipcub scan kernels, coarse, fine, scatter): every launch that runs
+// beside a batch accumulation costs it ~10-20 us, so the total,
+// the counter clears and the class scan ride in the kernels above instead of
+// launches of their own.
 //
 // fb_bits is chosen per problem so that there are ~256 coarse bins: few enough
 // that a tile's writes to one bin form runs of tens of entries (the L2 merges
@@ -29,11 +37,19 @@ constexpr int BS_TILE = 4096;         // entries per tile (256 threads x 16; sta
 constexpr int BS_MAX_FB_BITS = 12;    // fine buckets per coarse bin <= 4096 (2 x 16 KiB LDS)
 constexpr int BS_MAX_CB = 8192;       // coarse bins held in LDS (32 KiB)
 constexpr uint32_t BS_NONE = 0xffffffffu;
+// accumulation schedule classes (see k_sched_scatter): class = 255 - min(count, 255)
+constexpr int SCHED_PER_THREAD = 16;
+constexpr int SCHED_PER_BLOCK = 256 * SCHED_PER_THREAD;
+__device__ __forceinline__ uint32_t sched_class(uint32_t c) { return 255u - (c < 255u ? c : 255u); }
 
+// Block 0 also clears the schedule's class counters (SCHED_WORDS words), which
+// k_bs_fine and k_sched_scatter of this same sort use later in stream order.
 static __global__ void __launch_bounds__(256)
     k_bs_hist(const uint32_t *__restrict__ keys, size_t ne, int fb_bits, int ncb, int ntiles,
-              uint32_t *__restrict__ ghist) {
+              uint32_t *__restrict__ ghist, uint32_t *__restrict__ classes) {
   __shared__ uint32_t h[BS_MAX_CB];
+  if (blockIdx.x == 0)
+    for (int c = threadIdx.x; c < 512; c += blockDim.x) classes[c] = 0;
   for (int b = threadIdx.x; b < ncb; b += blockDim.x) h[b] = 0;
   __syncthreads();
   const size_t t0 = (size_t)blockIdx.x * BS_TILE;
@@ -182,20 +198,24 @@ constexpr int BS_FINE_MAXW = 8;
 
 static __global__ void __launch_bounds__(1024)
     k_bs_fine(const uint32_t *__restrict__ okeys, const uint32_t *__restrict__ ovals, int fb_bits, int ncb,
-              int ntiles, const uint32_t *__restrict__ gbase, const uint32_t *__restrict__ total, uint32_t nb,
-              uint32_t *__restrict__ sorted, uint32_t *__restrict__ counts, uint32_t *__restrict__ offsets) {
+              int ntiles, const uint32_t *__restrict__ gbase, const uint32_t *__restrict__ ghist, uint32_t nb,
+              uint32_t *__restrict__ sorted, uint32_t *__restrict__ counts, uint32_t *__restrict__ offsets,
+              uint32_t *__restrict__ class_total) {
   __shared__ uint32_t off[1 << BS_MAX_FB_BITS];
   __shared__ uint8_t win[1 << BS_MAX_FB_BITS];
   __shared__ uint32_t stage[BS_FINE_CAP];
   __shared__ uint32_t wsum[16];
   __shared__ uint32_t wb[BS_FINE_MAXW + 1];
+  __shared__ uint32_t cls[256];
   const int FB = 1 << fb_bits;
   const uint32_t fmask = (uint32_t)FB - 1u;
   const int b = blockIdx.x;
+  const size_t last = (size_t)ncb * ntiles - 1;  // the last (bin, tile) slot ends the valid entries
   const uint32_t lo = gbase[(size_t)b * ntiles];
-  const uint32_t hi = b + 1 < ncb ? gbase[(size_t)(b + 1) * ntiles] : *total;
+  const uint32_t hi = b + 1 < ncb ? gbase[(size_t)(b + 1) * ntiles] : gbase[last] + ghist[last];
   const uint32_t nbin = hi - lo;
   for (int f = threadIdx.x; f < FB; f += blockDim.x) off[f] = 0;
+  if (threadIdx.x < 256) cls[threadIdx.x] = 0;
   if (threadIdx.x <= BS_FINE_MAXW) wb[threadIdx.x] = nbin;
   __syncthreads();
   constexpr int U = 16, UW = 12;  // loads in flight per thread (histogram / window passes)
@@ -213,9 +233,13 @@ static __global__ void __launch_bounds__(1024)
   __syncthreads();
   for (int f = threadIdx.x; f < FB; f += blockDim.x) {
     uint32_t bucket = ((uint32_t)b << fb_bits) + f;
-    if (bucket < nb) counts[bucket] = off[f];
+    if (bucket < nb) {
+      counts[bucket] = off[f];
+      atomicAdd(&cls[sched_class(off[f])], 1u);  // the schedule's class histogram (was k_sched_hist)
+    }
   }
   __syncthreads();
+  if (threadIdx.x < 256 && cls[threadIdx.x]) atomicAdd(&class_total[threadIdx.x], cls[threadIdx.x]);
   block_exclusive_scan_4096(off, FB, wsum);
   const uint32_t nwin = (nbin + BS_FINE_STEP - 1) / BS_FINE_STEP;
   const bool staged = nwin <= (uint32_t)BS_FINE_MAXW;
@@ -281,56 +305,34 @@ static __global__ void __launch_bounds__(1024)
 }
 
 // ---- accumulation schedule: bucket ids ordered by entry count, descending ----
-// class = 255 - min(count, 255).  k_sched_hist: per-class totals (LDS histogram
-// per SCHED_PER_BLOCK buckets, one global atomic per non-empty class and block).
-// k_sched_scatter: each workgroup reserves its per-class ranges with one global
-// atomic per class and writes its bucket ids.  The order inside a class is
-// arbitrary.  A block covers 4096 buckets so that the ~20 busy class counters
-// see a few hundred atomics, not one per 256 buckets (a single address
-// saturates at ~88 atomics/us, MI355X_MICROARCH.md).
-constexpr int SCHED_PER_THREAD = 16;
-constexpr int SCHED_PER_BLOCK = 256 * SCHED_PER_THREAD;
-__device__ __forceinline__ uint32_t sched_class(uint32_t c) { return 255u - (c < 255u ? c : 255u); }
-
+// class = 255 - min(count, 255).  k_bs_fine accumulates the per-class totals
+// (an LDS histogram per coarse bin, one global atomic per non-empty class and
+// bin).  k_sched_scatter: every workgroup scans the 256 class totals in LDS
+// (exclusive class bases), reserves its per-class ranges with one global
+// atomic per class on the cursors class_total[256 + c], and writes its bucket
+// ids.  The order inside a class is arbitrary.  A block covers 4096 buckets so
+// that the ~20 busy class cursors see a few hundred atomics, not one per 256
+// buckets (a single address saturates at ~88 atomics/us, MI355X_MICROARCH.md).
 static __global__ void __launch_bounds__(256)
-    k_sched_hist(const uint32_t *__restrict__ counts, uint32_t nb, uint32_t *__restrict__ class_total) {
-  __shared__ uint32_t h[256];
-  const uint32_t t = threadIdx.x, b0 = blockIdx.x * SCHED_PER_BLOCK;
-  h[t] = 0;
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < SCHED_PER_THREAD; ++r) {
-    const uint32_t b = b0 + r * 256 + t;
-    if (b < nb) atomicAdd(&h[sched_class(counts[b])], 1u);
-  }
-  __syncthreads();
-  if (h[t]) atomicAdd(&class_total[t], h[t]);
-}
-// class_total -> exclusive class bases, in place (one wave)
-static __global__ void k_sched_scan(uint32_t *__restrict__ class_total) {
-  const int l = threadIdx.x;
-  uint32_t v0 = class_total[4 * l], v1 = class_total[4 * l + 1], v2 = class_total[4 * l + 2],
-           v3 = class_total[4 * l + 3];
-  uint32_t s = v0 + v1 + v2 + v3, incl = s;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    uint32_t v = __shfl_up(incl, d, 64);
-    if (l >= d) incl += v;
-  }
-  uint32_t base = incl - s;
-  class_total[4 * l] = base;
-  class_total[4 * l + 1] = base + v0;
-  class_total[4 * l + 2] = base + v0 + v1;
-  class_total[4 * l + 3] = base + v0 + v1 + v2;
-}
-static __global__ void __launch_bounds__(256)
-    k_sched_scatter(const uint32_t *__restrict__ counts, uint32_t nb, uint32_t *__restrict__ class_cursor,
+    k_sched_scatter(const uint32_t *__restrict__ counts, uint32_t nb, uint32_t *__restrict__ class_total,
                     uint32_t *__restrict__ order) {
   __shared__ uint32_t h[256];
   __shared__ uint32_t base[256];
-  const uint32_t t = threadIdx.x, b0 = blockIdx.x * SCHED_PER_BLOCK;
+  __shared__ uint32_t wsum[4];
+  const uint32_t t = threadIdx.x, b0 = blockIdx.x * SCHED_PER_BLOCK, lane = t & 63, wave = t >> 6;
   h[t] = 0;
+  // exclusive scan of the class totals: one value per thread, wave scans + 4 wave sums
+  const uint32_t v = class_total[t];
+  uint32_t incl = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t u = __shfl_up(incl, d, 64);
+    if (lane >= (uint32_t)d) incl += u;
+  }
+  if (lane == 63) wsum[wave] = incl;
   __syncthreads();
+  uint32_t cbase = incl - v;
+  for (uint32_t w = 0; w < wave; ++w) cbase += wsum[w];
   uint32_t cls[SCHED_PER_THREAD], rank[SCHED_PER_THREAD];
 #pragma unroll
   for (int r = 0; r < SCHED_PER_THREAD; ++r) {
@@ -339,7 +341,7 @@ static __global__ void __launch_bounds__(256)
     rank[r] = b < nb ? atomicAdd(&h[cls[r]], 1u) : 0u;
   }
   __syncthreads();
-  if (h[t]) base[t] = atomicAdd(&class_cursor[t], h[t]);
+  if (h[t]) base[t] = cbase + atomicAdd(&class_total[256 + t], h[t]);
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < SCHED_PER_THREAD; ++r) {
@@ -348,10 +350,5 @@ static __global__ void __launch_bounds__(256)
   }
 }
 
-// total number of valid entries = inclusive end of the last (bin, tile) slot
-static __global__ void k_bs_total(const uint32_t *__restrict__ gbase, const uint32_t *__restrict__ ghist,
-                                  size_t nslots, uint32_t *__restrict__ total) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) *total = gbase[nslots - 1] + ghist[nslots - 1];
-}
 
 }  // namespace msm

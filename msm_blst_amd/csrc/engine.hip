@@ -33,27 +33,22 @@ void BucketSort::run(hipStream_t s, const uint32_t *keys, const uint32_t *vals, 
   gbase.ensure(nslots * 4);
   okeys.ensure(std::max<size_t>(ne, 1) * 4);
   ovals.ensure(std::max<size_t>(ne, 1) * 4);
-  total.ensure(16);
   size_t scan_tmp = 0;
   hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, ghist.as<uint32_t>(), gbase.as<uint32_t>(), (int)nslots, s);
   tmp.ensure(scan_tmp);
-  hipLaunchKernelGGL(k_bs_hist, dim3(ntiles), dim3(256), 0, s, keys, ne, fb_bits, ncb, ntiles, ghist.as<uint32_t>());
+  classes.ensure(512 * 4);  // 256 class totals + 256 class cursors, cleared by k_bs_hist's block 0
+  hipLaunchKernelGGL(k_bs_hist, dim3(ntiles), dim3(256), 0, s, keys, ne, fb_bits, ncb, ntiles, ghist.as<uint32_t>(),
+                     classes.as<uint32_t>());
   MSM_HIP_CHECK(hipGetLastError());
   size_t tb = scan_tmp;
   MSM_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, ghist.as<uint32_t>(), gbase.as<uint32_t>(), (int)nslots, s));
-  hipLaunchKernelGGL(k_bs_total, dim3(1), dim3(64), 0, s, gbase.as<uint32_t>(), ghist.as<uint32_t>(), nslots,
-                     total.as<uint32_t>());
   hipLaunchKernelGGL(k_bs_coarse, dim3(ntiles), dim3(256), (size_t)(2 * ncb + 2 * BS_TILE) * 4, s, keys, vals, ne,
                      fb_bits, ncb, ntiles, gbase.as<uint32_t>(), okeys.as<uint32_t>(), ovals.as<uint32_t>());
   MSM_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(k_bs_fine, dim3(ncb), dim3(1024), 0, s, okeys.as<uint32_t>(), ovals.as<uint32_t>(), fb_bits, ncb,
-                     ntiles, gbase.as<uint32_t>(), total.as<uint32_t>(), nb, sorted, counts, offsets);
-  MSM_HIP_CHECK(hipGetLastError());
-  classes.ensure(256 * 4);
-  MSM_HIP_CHECK(hipMemsetAsync(classes.p, 0, 256 * 4, s));
-  hipLaunchKernelGGL(k_sched_hist, dim3(nblk(nb, SCHED_PER_BLOCK)), dim3(256), 0, s, counts, nb,
+                     ntiles, gbase.as<uint32_t>(), ghist.as<uint32_t>(), nb, sorted, counts, offsets,
                      classes.as<uint32_t>());
-  hipLaunchKernelGGL(k_sched_scan, dim3(1), dim3(64), 0, s, classes.as<uint32_t>());
+  MSM_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(k_sched_scatter, dim3(nblk(nb, SCHED_PER_BLOCK)), dim3(256), 0, s, counts, nb,
                      classes.as<uint32_t>(), order);
   MSM_HIP_CHECK(hipGetLastError());

@@ -67,7 +67,7 @@ struct HostField<2> {
 // Produces payloads grouped by bucket, per-bucket counts/offsets and the
 // accumulation schedule (bucket ids by descending count).
 struct BucketSort {
-  DevBuf ghist, gbase, okeys, ovals, total, classes, tmp;
+  DevBuf ghist, gbase, okeys, ovals, classes, tmp;
   // keys[ne] (bucket < nb or 0xffffffff), vals[ne]; outputs sized ne / nb
   void run(hipStream_t s, const uint32_t *keys, const uint32_t *vals, size_t ne, uint32_t nb, uint32_t *sorted,
            uint32_t *counts, uint32_t *offsets, uint32_t *order);

@@ -13,6 +13,9 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 import msm_blst_amd as m  # noqa: E402
 
+if os.environ.get("MSM_LIB"):  # A/B of two builds on one box (e.g. tools/ablib/libmsm_prev.so)
+    m._ffi.LIB_PATH = os.environ["MSM_LIB"]
+
 K = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 R = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 n = 1 << 20
