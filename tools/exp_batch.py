@@ -44,3 +44,16 @@ for name, ptr, ondev in (("resident", d_all.data_ptr(), True), ("h2d", host.data
     print(f"EXP {name}: {n * K / best / 1e6:.1f} M pairs/s "
           f"({best / K * 1e3:.3f} ms/MSM, acc {ctx.phase_times()['accumulate']:.3f} ms) same={ok} runs={[round(x) for x in runs]}",
           flush=True)
+
+if os.environ.get("EXP_SYNC"):
+    best = 1e9
+    for r in range(R):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for k in range(K):
+            ctx.mult(d_all.data_ptr() + k * n * 32, 32, on_device=True, stream=sp)
+        torch.cuda.synchronize()
+        best = min(best, time.perf_counter() - t)
+    ph = ctx.phase_times()
+    print(f"EXP sync: {n * K / best / 1e6:.1f} M pairs/s ({best / K * 1e3:.3f} ms/MSM) "
+          f"phases {{{', '.join(f'{k}: {v:.3f}' for k, v in ph.items())}}}", flush=True)
