@@ -234,6 +234,57 @@ void WeightedReducer<G>::plan(const std::vector<uint32_t> &w, const std::vector<
     C = 2;
     if (cur_seg.empty()) break;
   }
+  // bit phase (sync tail of one-window plans): segment (block, j) over the
+  // final partials p of block = cur_seg[p] / S whose value cur_seg[p] % S + 1
+  // has bit j; chunks of 8, pairwise levels, then a scatter to 2 s slots
+  std::vector<uint32_t> bidx;
+  bits_ = nwin == 1;
+  bstarts_.clear();
+  bnout_.clear();
+  if (bits_) {
+    const uint32_t NB2 = 2u * (uint32_t)nwin * (uint32_t)sbits_;
+    std::vector<uint32_t> bseg;
+    for (uint32_t bs = 0; bs < NB2; ++bs) {
+      const uint32_t blk = bs / (uint32_t)sbits_, j = bs % (uint32_t)sbits_;
+      for (size_t q = 0; q < cur_seg.size(); ++q)
+        if (cur_seg[q] / S == blk && (((cur_seg[q] % S) + 1) >> j & 1u)) bidx.push_back((uint32_t)q), bseg.push_back(bs);
+    }
+    int Cb = 8;
+    while (!bseg.empty()) {
+      std::vector<uint32_t> st, nseg;
+      size_t k = 0;
+      while (k < bseg.size()) {
+        st.push_back((uint32_t)k);
+        nseg.push_back(bseg[k]);
+        size_t e = k + 1;
+        while (e < bseg.size() && e - k < (size_t)Cb && bseg[e] == bseg[k]) ++e;
+        k = e;
+      }
+      st.push_back((uint32_t)bseg.size());
+      if (!bnout_.empty() && nseg.size() == bseg.size()) break;
+      bstarts_.emplace_back();
+      bstarts_.back().ensure(st.size() * 4);
+      MSM_HIP_CHECK(hipMemcpy(bstarts_.back().p, st.data(), st.size() * 4, hipMemcpyHostToDevice));
+      bnout_.push_back(nseg.size());
+      bseg.swap(nseg);
+      Cb = 2;
+    }
+    std::vector<uint32_t> bdst(NB2 + 1, 0), bperm;
+    std::vector<int> bat(NB2, -1);
+    for (size_t k = 0; k < bseg.size(); ++k) bat[bseg[k]] = (int)k;
+    for (uint32_t sl = 0; sl < NB2; ++sl) {
+      bdst[sl] = (uint32_t)bperm.size();
+      if (bat[sl] >= 0) bperm.push_back((uint32_t)bat[sl]);
+    }
+    bdst[NB2] = (uint32_t)bperm.size();
+    bstarts_.emplace_back();
+    bstarts_.back().ensure(bdst.size() * 4);
+    MSM_HIP_CHECK(hipMemcpy(bstarts_.back().p, bdst.data(), bdst.size() * 4, hipMemcpyHostToDevice));
+    bnout_.push_back(NB2);
+    bidx.insert(bidx.end(), bperm.begin(), bperm.end());
+    bperm_off_ = bidx.size() - bperm.size();
+    bfin_.ensure((size_t)NB2 * 144 * G);
+  }
   // dense scatter: slot -> its single partial (or empty), via a permutation
   const size_t NS = (size_t)2 * nwin * S;
   std::vector<uint32_t> dst(NS + 1, 0), perm;
@@ -248,13 +299,17 @@ void WeightedReducer<G>::plan(const std::vector<uint32_t> &w, const std::vector<
   starts_.back().ensure(dst.size() * 4);
   MSM_HIP_CHECK(hipMemcpy(starts_.back().p, dst.data(), dst.size() * 4, hipMemcpyHostToDevice));
   nout_.push_back(NS);
-  std::vector<uint32_t> all = idx;  // [level-0 item list | final permutation]
+  std::vector<uint32_t> all = idx;  // [level-0 item list | final permutation | bit phase items | bit permutation]
   all.insert(all.end(), perm.begin(), perm.end());
+  final_perm_off_ = idx.size();
+  bidx_off_ = all.size();
+  bperm_off_ += bidx_off_;
+  all.insert(all.end(), bidx.begin(), bidx.end());
   idx_.ensure(std::max<size_t>(all.size(), 1) * 4);
   if (!all.empty()) MSM_HIP_CHECK(hipMemcpy(idx_.p, all.data(), all.size() * 4, hipMemcpyHostToDevice));
-  final_perm_off_ = idx.size();
   maxp_ = 1;
   for (size_t l = 0; l + 1 < nout_.size(); ++l) maxp_ = std::max(maxp_, nout_[l]);
+  for (size_t l = 0; l + 1 < bnout_.size(); ++l) maxp_ = std::max(maxp_, bnout_[l]);  // bit phase levels
   for (int st = 0; st < NSETS; ++st) {  // a new plan: sets are (re)sized on their next use
     part_[st][0].release();
     part_[st][1].release();
@@ -289,6 +344,39 @@ void WeightedReducer<G>::launch_tail(hipStream_t s, int set, bool coop) {
   typedef typename FieldOf<G>::F F;
   const size_t L = nout_.size();
   const Xyzz<F> *src = part_[set][0].as<Xyzz<F>>();
+  if (bits_ && L >= 2) {
+    // phase-1 levels 1 .. L-2 (level L-1 is the dense scatter, not used here),
+    // then the bit phase: its level 0 reads the final partials through the
+    // bit item list, later levels are contiguous, the last scatters to 2 s slots
+    int cur = 0;
+    auto segsum = [&](const Xyzz<F> *a, const uint32_t *ix, const uint32_t *st, Xyzz<F> *d, size_t nout) {
+      if (!nout) return;
+      if (G == 1 && coop && nout <= 16384)
+        hipLaunchKernelGGL(k_segsum_c<G>, dim3(nblk(nout, 64)), dim3(256), 0, s, a, ix, st, d, nout);
+      else
+        launch_segsum<G>(s, a, ix, st, d, nout);
+      MSM_HIP_CHECK(hipGetLastError());
+    };
+    for (size_t l = 1; l + 1 < L; ++l) {
+      Xyzz<F> *dst = part_[set][l & 1].as<Xyzz<F>>();
+      segsum(src, nullptr, starts_[l].as<uint32_t>(), dst, nout_[l]);
+      src = dst;
+      cur = (int)(l & 1);
+    }
+    const size_t LB = bnout_.size();
+    for (size_t l = 0; l < LB; ++l) {
+      const bool last = l + 1 == LB;
+      Xyzz<F> *dst = last ? dense_buf_[set].as<Xyzz<F>>() : part_[set][cur ^ 1].as<Xyzz<F>>();
+      const uint32_t *ix = l == 0 ? idx_.as<uint32_t>() + bidx_off_ : last ? idx_.as<uint32_t>() + bperm_off_ : nullptr;
+      segsum(src, ix, bstarts_[l].as<uint32_t>(), dst, bnout_[l]);
+      src = dst;
+      cur ^= 1;
+    }
+    hipLaunchKernelGGL(k_finalize<G>, dim3(nblk(bit_slots(), 64)), dim3(64), 0, s, src, bfin_.as<uint64_t>(),
+                       (int)bit_slots());
+    MSM_HIP_CHECK(hipGetLastError());
+    return;
+  }
   for (size_t l = 1; l < L; ++l) {
     const bool last = l + 1 == L;
     Xyzz<F> *dst = last ? dense_buf_[set].as<Xyzz<F>>() : part_[set][l & 1].as<Xyzz<F>>();
@@ -366,6 +454,23 @@ std::vector<hfp::Jac<typename HostField<G>::F>> WeightedReducer<G>::combine(cons
 
 template <int G>
 std::vector<hfp::Jac<typename HostField<G>::F>> WeightedReducer<G>::read_windows(hipStream_t s) {
+  if (bits_ && nout_.size() >= 2) {  // launch_tail's bit sums: T = sum_j 2^j B_j, Horner from the top bit
+    std::vector<hfp::Jac<HF>> B(bit_slots());
+    MSM_HIP_CHECK(hipMemcpyAsync(B.data(), bfin_.p, bit_slots() * sizeof(hfp::Jac<HF>), hipMemcpyDeviceToHost, s));
+    MSM_HIP_CHECK(hipStreamSynchronize(s));
+    std::vector<hfp::Jac<HF>> out(nwin_);
+    for (int ww = 0; ww < nwin_; ++ww) {
+      // bit j of the window's weight: low half block 2 ww (j < s), high half block 2 ww + 1
+      const hfp::Jac<HF> *lo = &B[(size_t)2 * ww * sbits_], *hi = lo + sbits_;
+      hfp::Jac<HF> acc = hi[sbits_ - 1];
+      for (int j = 2 * sbits_ - 2; j >= 0; --j) {
+        acc = hfp::dbl(acc);
+        acc = hfp::addj(acc, j >= sbits_ ? hi[j - sbits_] : lo[j]);
+      }
+      out[ww] = acc;
+    }
+    return out;
+  }
   std::vector<uint8_t> host(out_bytes());
   copy_out(s, 0, host.data());
   MSM_HIP_CHECK(hipStreamSynchronize(s));

@@ -175,12 +175,23 @@ class WeightedReducer {
 
  private:
   size_t dense_slots() const { return (size_t)2 * nwin_ << sbits_; }
+  size_t bit_slots() const { return (size_t)2 * nwin_ * sbits_; }
   size_t bsize_ = 0, final_perm_off_ = 0, maxp_ = 1;
   int sbits_ = 1, nwin_ = 1;
   DevBuf idx_, dense_buf_[NSETS], part_[NSETS][2];
   std::vector<DevBuf> starts_;
   std::vector<size_t> nout_;
   ScanReducer<G> dense_[NSETS];
+  // Synchronous tail of a one-window plan (launch_tail / read_windows): the
+  // dense 2 x 2^s stage (2 s dependent levels) is replaced by 2 s bit sums
+  // B_j = sum of the partials whose value has bit j (j < s: low half, j >= s:
+  // high half), ~log2(2^s s / 8) + 2 levels, and a 2 s-step host Horner
+  // (T = sum_j 2^j B_j).  Batch groups keep the dense stage (one per group).
+  bool bits_ = false;
+  size_t bidx_off_ = 0, bperm_off_ = 0;
+  std::vector<DevBuf> bstarts_;
+  std::vector<size_t> bnout_;
+  DevBuf bfin_;
 };
 
 // Plain Pippenger bucket method (ref src/multi_scalar.c:549-576) on one GPU.
