@@ -283,6 +283,7 @@ void WeightedReducer<G>::plan(const std::vector<uint32_t> &w, const std::vector<
     bnout_.push_back(NB2);
     bidx.insert(bidx.end(), bperm.begin(), bperm.end());
     bperm_off_ = bidx.size() - bperm.size();
+    bfin_.ensure((size_t)NB2 * 144 * G);
   }
   // dense scatter: slot -> its single partial (or empty), via a permutation
   const size_t NS = (size_t)2 * nwin * S;
@@ -324,7 +325,6 @@ void WeightedReducer<G>::ensure_set(int set) {
   part_[set][0].ensure(maxp_ * sizeof(Xyzz<F>));
   part_[set][1].ensure(maxp_ * sizeof(Xyzz<F>));
   dense_buf_[set].ensure((size_t)2 * nwin_ * ((size_t)1 << sbits_) * sizeof(Xyzz<F>));
-  if (bits_) bfin_[set].ensure(bit_slots() * 144 * G);
 }
 
 template <int G>
@@ -336,38 +336,6 @@ void WeightedReducer<G>::launch_head(hipStream_t s, const void *Sbuf, int set) {
   Xyzz<F> *dst = L == 1 ? dense_buf_[set].as<Xyzz<F>>() : part_[set][0].as<Xyzz<F>>();
   const uint32_t *ix = L == 1 ? idx_.as<uint32_t>() + final_perm_off_ : idx_.as<uint32_t>();
   launch_segsum<G>(s, src, ix, starts_[0].as<uint32_t>(), dst, nout_[0]);
-  MSM_HIP_CHECK(hipGetLastError());
-}
-
-// the bit phase for nmsm MSMs of buffer set `set` whose final segment partials
-// are at src (stride maxp_ per MSM); `cur` = the part_ buffer src lives in.
-// Output: nmsm x bit_slots() blst Jacobians in bfin_[set].
-template <int G>
-void WeightedReducer<G>::launch_bits(hipStream_t s, int set, int nmsm, const void *partials, int cur) {
-  typedef typename FieldOf<G>::F F;
-  const Xyzz<F> *src = reinterpret_cast<const Xyzz<F> *>(partials);
-  const size_t LB = bnout_.size(), NB2 = bit_slots();
-  bfin_[set].ensure((size_t)nmsm * NB2 * 144 * G);
-  size_t sstride = maxp_;
-  for (size_t l = 0; l < LB; ++l) {
-    const bool last = l + 1 == LB;
-    Xyzz<F> *dst = last ? dense_buf_[set].as<Xyzz<F>>() : part_[set][cur ^ 1].as<Xyzz<F>>();
-    const uint32_t *ix = l == 0 ? idx_.as<uint32_t>() + bidx_off_ : last ? idx_.as<uint32_t>() + bperm_off_ : nullptr;
-    const size_t dstride = last ? NB2 : maxp_;
-    if (bnout_[l]) {
-      if (G == 1 && nmsm == 1 && bnout_[l] <= 16384)  // latency-bound levels of one MSM: 4 waves per add
-        hipLaunchKernelGGL(k_segsum_c<G>, dim3(nblk(bnout_[l], 64)), dim3(256), 0, s, src, ix,
-                           bstarts_[l].as<uint32_t>(), dst, bnout_[l]);
-      else
-        launch_segsum<G>(s, src, ix, bstarts_[l].as<uint32_t>(), dst, bnout_[l], nmsm, sstride, dstride);
-      MSM_HIP_CHECK(hipGetLastError());
-    }
-    src = dst;
-    sstride = dstride;
-    cur ^= 1;
-  }
-  hipLaunchKernelGGL(k_finalize<G>, dim3(nblk((size_t)nmsm * NB2, 64)), dim3(64), 0, s, src, bfin_[set].as<uint64_t>(),
-                     (int)((size_t)nmsm * NB2));
   MSM_HIP_CHECK(hipGetLastError());
 }
 
@@ -395,7 +363,18 @@ void WeightedReducer<G>::launch_tail(hipStream_t s, int set, bool coop) {
       src = dst;
       cur = (int)(l & 1);
     }
-    launch_bits(s, set, 1, src, cur);
+    const size_t LB = bnout_.size();
+    for (size_t l = 0; l < LB; ++l) {
+      const bool last = l + 1 == LB;
+      Xyzz<F> *dst = last ? dense_buf_[set].as<Xyzz<F>>() : part_[set][cur ^ 1].as<Xyzz<F>>();
+      const uint32_t *ix = l == 0 ? idx_.as<uint32_t>() + bidx_off_ : last ? idx_.as<uint32_t>() + bperm_off_ : nullptr;
+      segsum(src, ix, bstarts_[l].as<uint32_t>(), dst, bnout_[l]);
+      src = dst;
+      cur ^= 1;
+    }
+    hipLaunchKernelGGL(k_finalize<G>, dim3(nblk(bit_slots(), 64)), dim3(64), 0, s, src, bfin_.as<uint64_t>(),
+                       (int)bit_slots());
+    MSM_HIP_CHECK(hipGetLastError());
     return;
   }
   for (size_t l = 1; l < L; ++l) {
@@ -426,7 +405,6 @@ void WeightedReducer<G>::ensure_group(int set, int nmsm) {
   dense_[set].buf[0].ensure(NT * sizeof(Xyzz<F>));
   dense_[set].buf[1].ensure(NT * sizeof(Xyzz<F>));
   dense_[set].fin.ensure((size_t)nmsm * out_bytes());
-  if (bits_) bfin_[set].ensure((size_t)nmsm * bit_slots() * 144 * G);
 }
 
 template <int G>
@@ -445,18 +423,6 @@ void WeightedReducer<G>::launch_tail_group(hipStream_t s, int set, int nmsm) {
   typedef typename FieldOf<G>::F F;
   const size_t L = nout_.size();
   const Xyzz<F> *src = part_[set][0].as<Xyzz<F>>();
-  if (bits_ && L >= 2) {  // segment levels 1 .. L-2, then the bit phase (no dense stage)
-    int cur = 0;
-    for (size_t l = 1; l + 1 < L; ++l) {
-      Xyzz<F> *dst = part_[set][l & 1].as<Xyzz<F>>();
-      launch_segsum<G>(s, src, nullptr, starts_[l].as<uint32_t>(), dst, nout_[l], nmsm, maxp_, maxp_);
-      MSM_HIP_CHECK(hipGetLastError());
-      src = dst;
-      cur = (int)(l & 1);
-    }
-    launch_bits(s, set, nmsm, src, cur);
-    return;
-  }
   for (size_t l = 1; l < L; ++l) {
     const bool last = l + 1 == L;
     Xyzz<F> *dst = last ? dense_buf_[set].as<Xyzz<F>>() : part_[set][l & 1].as<Xyzz<F>>();
@@ -470,8 +436,7 @@ void WeightedReducer<G>::launch_tail_group(hipStream_t s, int set, int nmsm) {
 
 template <int G>
 void WeightedReducer<G>::copy_out_group(hipStream_t s, int set, int nmsm, void *host) {
-  const void *src = bits_ && nout_.size() >= 2 ? bfin_[set].p : dense_[set].fin.p;
-  MSM_HIP_CHECK(hipMemcpyAsync(host, src, (size_t)nmsm * out_bytes(), hipMemcpyDeviceToHost, s));
+  MSM_HIP_CHECK(hipMemcpyAsync(host, dense_[set].fin.p, (size_t)nmsm * out_bytes(), hipMemcpyDeviceToHost, s));
 }
 
 template <int G>
@@ -483,10 +448,20 @@ template <int G>
 std::vector<hfp::Jac<typename HostField<G>::F>> WeightedReducer<G>::combine(const void *host) const {
   const hfp::Jac<HF> *T = reinterpret_cast<const hfp::Jac<HF> *>(host);
   std::vector<hfp::Jac<HF>> out(nwin_);
-  if (bits_ && nout_.size() >= 2) {  // 2 s bit sums per window: T = sum_j 2^j B_j, Horner from the top bit
+  for (int ww = 0; ww < nwin_; ++ww) out[ww] = horner(std::vector<hfp::Jac<HF>>{T[2 * ww], T[2 * ww + 1]}, sbits_);
+  return out;
+}
+
+template <int G>
+std::vector<hfp::Jac<typename HostField<G>::F>> WeightedReducer<G>::read_windows(hipStream_t s) {
+  if (bits_ && nout_.size() >= 2) {  // launch_tail's bit sums: T = sum_j 2^j B_j, Horner from the top bit
+    std::vector<hfp::Jac<HF>> B(bit_slots());
+    MSM_HIP_CHECK(hipMemcpyAsync(B.data(), bfin_.p, bit_slots() * sizeof(hfp::Jac<HF>), hipMemcpyDeviceToHost, s));
+    MSM_HIP_CHECK(hipStreamSynchronize(s));
+    std::vector<hfp::Jac<HF>> out(nwin_);
     for (int ww = 0; ww < nwin_; ++ww) {
       // bit j of the window's weight: low half block 2 ww (j < s), high half block 2 ww + 1
-      const hfp::Jac<HF> *lo = T + (size_t)2 * ww * sbits_, *hi = lo + sbits_;
+      const hfp::Jac<HF> *lo = &B[(size_t)2 * ww * sbits_], *hi = lo + sbits_;
       hfp::Jac<HF> acc = hi[sbits_ - 1];
       for (int j = 2 * sbits_ - 2; j >= 0; --j) {
         acc = hfp::dbl(acc);
@@ -495,18 +470,6 @@ std::vector<hfp::Jac<typename HostField<G>::F>> WeightedReducer<G>::combine(cons
       out[ww] = acc;
     }
     return out;
-  }
-  for (int ww = 0; ww < nwin_; ++ww) out[ww] = horner(std::vector<hfp::Jac<HF>>{T[2 * ww], T[2 * ww + 1]}, sbits_);
-  return out;
-}
-
-template <int G>
-std::vector<hfp::Jac<typename HostField<G>::F>> WeightedReducer<G>::read_windows(hipStream_t s) {
-  if (bits_ && nout_.size() >= 2) {  // launch_tail's bit sums
-    std::vector<uint8_t> host(out_bytes());
-    MSM_HIP_CHECK(hipMemcpyAsync(host.data(), bfin_[0].p, out_bytes(), hipMemcpyDeviceToHost, s));
-    MSM_HIP_CHECK(hipStreamSynchronize(s));
-    return combine(host.data());
   }
   std::vector<uint8_t> host(out_bytes());
   copy_out(s, 0, host.data());
@@ -543,7 +506,6 @@ Ches<G>::~Ches() {
   for (auto &e : ev_) (void)hipEventDestroy(e);
   for (auto &e : acc_ev_) (void)hipEventDestroy(e);
   for (auto &e : bev_) (void)hipEventDestroy(e);
-  for (auto &e : gev_) (void)hipEventDestroy(e);
   for (int t = 0; t < kBSets; ++t) {
     if (ev_tail_[t]) (void)hipEventDestroy(ev_tail_[t]);
     if (tails_[t]) (void)hipStreamDestroy(tails_[t]);
@@ -820,11 +782,6 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
   // No host waits inside the loop: every MSM has its own pinned read-back slot.
   // Reducer set t is reused by group g + 2 only after group g's tail: both are
   // in order on tails_[t].
-  while (gev_.size() < ngroups) {
-    hipEvent_t e;
-    MSM_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    gev_.push_back(e);
-  }
   while (bev_.size() < 4 * count + 1) {
     hipEvent_t e;
     MSM_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -869,7 +826,6 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
     if ((size_t)slot + 1 == R || k + 1 == count) {  // the group's last MSM
       red_.launch_tail_group(ts, gset, slot + 1);
       red_.copy_out_group(ts, gset, slot + 1, (uint8_t *)host_out_ + (k - slot) * ob);
-      MSM_HIP_CHECK(hipEventRecord(gev_[k / R], ts));
     }
   }
   // the caller's stream observes completion of every reduction (and front)
@@ -877,14 +833,8 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
     MSM_HIP_CHECK(hipEventRecord(ev_tail_[t], tails_[t]));
     MSM_HIP_CHECK(hipStreamWaitEvent(s, ev_tail_[t], 0));
   }
-  // host Horner of each group as soon as its read-back lands, while the GPU
-  // still reduces the later groups
-  for (size_t g = 0; g < ngroups; ++g) {
-    MSM_HIP_CHECK(hipEventSynchronize(gev_[g]));
-    for (size_t k = g * R; k < std::min(count, (g + 1) * R); ++k)
-      outs[k] = red_.combine((const uint8_t *)host_out_ + k * ob)[0];
-  }
   for (int t = 0; t < kBSets; ++t) MSM_HIP_CHECK(hipStreamSynchronize(tails_[t]));
+  for (size_t k = 0; k < count; ++k) outs[k] = red_.combine((const uint8_t *)host_out_ + k * ob)[0];
   profile_ = prof;
   if (prof) {  // average accumulation time over the batch (HIP events on stream s)
     float sum = 0;

@@ -154,8 +154,7 @@ class WeightedReducer {
     launch_head(s, S, 0);
     launch_tail(s, 0);
   }
-  // host bytes of one MSM's read-back: 2 s bit sums (bit plans) or 2 nwin dense window halves
-  size_t out_bytes() const { return (bits_ ? bit_slots() : (size_t)2 * nwin_) * 144 * G; }
+  size_t out_bytes() const { return (size_t)2 * nwin_ * 144 * G; }
   void copy_out(hipStream_t s, int set, void *host);               // async D2H of out_bytes()
   std::vector<hfp::Jac<HF>> combine(const void *host) const;        // per-window sums
   std::vector<hfp::Jac<HF>> read_windows(hipStream_t s);            // set 0, waits
@@ -183,17 +182,16 @@ class WeightedReducer {
   std::vector<DevBuf> starts_;
   std::vector<size_t> nout_;
   ScanReducer<G> dense_[NSETS];
-  // Tail of a one-window plan (launch_tail, launch_tail_group): the dense
-  // 2 x 2^s stage (2 s dependent levels) is replaced by 2 s bit sums B_j = sum
-  // of the partials whose value has bit j (j < s: low half, j >= s: high
-  // half), ~log2(2^s s / 8) + 2 levels, and a 2 s-step host Horner
-  // (combine: T = sum_j 2^j B_j).
+  // Synchronous tail of a one-window plan (launch_tail / read_windows): the
+  // dense 2 x 2^s stage (2 s dependent levels) is replaced by 2 s bit sums
+  // B_j = sum of the partials whose value has bit j (j < s: low half, j >= s:
+  // high half), ~log2(2^s s / 8) + 2 levels, and a 2 s-step host Horner
+  // (T = sum_j 2^j B_j).  Batch groups keep the dense stage (one per group).
   bool bits_ = false;
   size_t bidx_off_ = 0, bperm_off_ = 0;
   std::vector<DevBuf> bstarts_;
   std::vector<size_t> bnout_;
-  DevBuf bfin_[NSETS];
-  void launch_bits(hipStream_t s, int set, int nmsm, const void *partials, int cur);
+  DevBuf bfin_;
 };
 
 // Plain Pippenger bucket method (ref src/multi_scalar.c:549-576) on one GPU.
@@ -295,7 +293,6 @@ class Ches {
   void *host_out_ = nullptr;
   size_t host_out_bytes_ = 0;
   std::vector<hipEvent_t> bev_;     // batch dependency events, one per (MSM, stage)
-  std::vector<hipEvent_t> gev_;     // batch: one per reduction group, after its read-back
   std::vector<hipEvent_t> acc_ev_;  // batch profiling: events around each accumulation
   void digits_sort(hipStream_t s, const uint8_t *d_scalars, size_t stride, int set);
   void accumulate(hipStream_t s, int set, int bset);
