@@ -49,7 +49,7 @@ FPMUL_PEAK = 76.8e9            # measured register-resident Fp-mul/s: profiles/r
 AFFINE_BYTES = 96              # one G1 affine point (blst layout), SURVEY 8d
 FPMUL_PER_MADD = 10            # 8M + 2S (ec_ops.h:727-748)
 CPU_THREADS = 16               # the GPU box's CPU share per GPU (16 threads)
-DEFAULT_BETA = {}              # log_n -> ches_config_files variant used by default (measured on MI355X)
+DEFAULT_BETA = {}              # log_n -> ches_config_files variant used by default; _beta at 2^20 measured slower
 
 
 def log(*a):
