@@ -384,7 +384,11 @@ def main():
                           "peak": round(FPMUL_PEAK / 1e9, 2), "unit": "G Fp-mul/s",
                           "frac": round(fpmul_rate / FPMUL_PEAK, 4),
                           "work": f"{madds} xyzz madds x {fpm_per_madd} Fp-mul",
-                          "peak_basis": "measured register-resident Fp-mul kernel (profiles/r02_fp_rate.txt)"},
+                          "peak_basis": "measured register-resident Fp-mul kernel (profiles/r02_fp_rate.txt)",
+                          "frac_alone": (round(madds * fpm_per_madd / (phases["accumulate"] / 1e3) / FPMUL_PEAK, 4)
+                                         if phases.get("accumulate") else None),
+                          "alone_basis": "the same kernel in one synchronous MSM (phases_ms.accumulate): no front or "
+                                         "reduction of a neighbouring MSM shares its SIMDs"},
         "phases_ms": {k: round(v, 4) for k, v in phases.items()},
         "phases_note": "one synchronous MSM (profiled) after the timed region" if batched else "last timed step",
         "pipelined_batch": batched,
