@@ -128,6 +128,8 @@ def main():
     ap.add_argument("--no-batch", action="store_true",
                     help="CHES: time K independent synchronous MSMs instead of one pipelined batch of K")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the other BASELINE configs' legs (configs[0], [1], [4], the blst drop-in at 2^20)")
     ap.add_argument("--cpu-sample-log-n", type=int, default=20)
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
@@ -307,6 +309,9 @@ def main():
                              "parity_vs_reference": (m.compress(G, ores[0]).hex() == want[0]) if want else None}
             octx.close()
 
+    if world == 1 and not args.no_compare and not args.no_configs and G == 1 and args.log_n == 20:
+        others.update(config_legs(m, torch, dev, local, sp, pts, host, K, W))
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(m, pts, host, n, K, res, G, args.cpu_sample_log_n if G == 1 else min(args.cpu_sample_log_n, 18))
@@ -401,6 +406,172 @@ def main():
     print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+def _golden(m, G, n):
+    gold = json.load(open(os.path.join(REPO, "tests", "golden", f"msm_g{G}.json")))
+    want = [c["compressed"] for c in gold["cases"] if c["n"] == n and c["seed"] == 1 and c["case"] == "rand"
+            and c["nbits"] == 255]
+    return want[0] if want else None
+
+
+def config_legs(m, torch, dev, local, sp, pts, host, K, W):
+    """The other single-GPU BASELINE configs and the blst drop-in boundary, each
+    timed and parity-checked against the reference's golden (set 0 = the seed-1
+    stream, whose first 2^k scalars are the seed-1 set of 2^k points):
+      configs[1]  G1 n=2^16 plain Pippenger: device-resident context (scalar sets
+                  resident) and the blst drop-in blst_p1s_mult_pippenger (points
+                  and scalars in the caller's pageable host memory, per call)
+      boundary    blst_p1s_mult_pippenger at n=2^20 (the north star's
+                  pippenger_blst_built_in, main_p1.cpp:400-436), per call
+      configs[4]  G2 n=2^20 CHES batch (table resident), scalars H2D / resident
+      configs[0]  G1 n=2^10 on the CPU: the reference's blst_p1s_mult_pippenger
+                  (oracle/_ref), beside the GPU drop-in at the same size"""
+    import numpy as np
+    legs = {}
+    hv = host.numpy()
+    nsets = host.numel() // (32 << 20)
+
+    def set_bytes(k, n):  # first n scalars of set k, in fresh pageable host memory
+        off = (k % nsets) * (32 << 20)
+        return (ctypes.c_uint8 * (32 * n)).from_buffer_copy(hv[off:off + 32 * n].tobytes())
+
+    def dropin(G, P, S, n):
+        pp = (ctypes.c_void_p * 2)(ctypes.cast(P, ctypes.c_void_p), None)
+        spp = (ctypes.c_void_p * 2)(ctypes.cast(S, ctypes.c_void_p), None)
+        r = (ctypes.c_uint8 * (144 * G))()
+        getattr(m.lib(), f"blst_p{G}s_mult_pippenger")(r, pp, n, spp, 255, None)
+        return bytes(r)
+
+    def timed(fn, k):
+        torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        out = [fn(i) for i in range(k)]
+        torch.cuda.synchronize(dev)
+        return out, time.perf_counter() - t
+
+    # ---- configs[1]: G1 2^16 plain Pippenger ----
+    n16 = 1 << 16
+    P16 = (ctypes.c_uint8 * (96 * n16)).from_buffer_copy(bytes(pts)[:96 * n16])
+    want16 = _golden(m, 1, n16)
+    sets16 = [set_bytes(k, n16) for k in range(K)]
+    d16 = torch.tensor(np.frombuffer(b"".join(bytes(x) for x in sets16), dtype=np.uint8), device=dev)
+    for c in (12, 13):
+        pc = m.MSMContext(1, local, c)
+        pc.set_points(P16, n16, stream=sp)
+        pc.mult(d16.data_ptr(), 255, stride=32, on_device=True, stream=sp)
+        r, el = timed(lambda k: pc.mult(d16.data_ptr() + k * 32 * n16, 255, stride=32, on_device=True, stream=sp), K)
+        pc.set_profiling(True)
+        pc.mult(d16.data_ptr(), 255, stride=32, on_device=True, stream=sp)
+        legs[f"cfg1_pippenger_2^16_ctx_c{c}"] = {
+            "value": round(n16 * K / el, 1), "unit": "pairs/s", "ms_per_step": round(el / K * 1e3, 4),
+            "phases_ms": {kk: round(v, 4) for kk, v in pc.phase_times().items()},
+            "parity_vs_reference": m.compress(1, r[0]).hex() == want16,
+            "note": f"configs[1]: msm_ctx_mult, window c={c}, points and {K} scalar sets resident in HBM"}
+        pc.close()
+    for _ in range(max(W, 1)):
+        dropin(1, P16, sets16[0], n16)
+    r, el = timed(lambda k: dropin(1, P16, sets16[k], n16), K)
+    legs["cfg1_pippenger_2^16_blst_dropin"] = {
+        "value": round(n16 * K / el, 1), "unit": "pairs/s", "ms_per_step": round(el / K * 1e3, 4),
+        "parity_vs_reference": m.compress(1, r[0]).hex() == want16,
+        "note": "configs[1] through blst_p1s_mult_pippenger: {ptr, NULL} arrays in pageable host memory, points and "
+                "scalars uploaded by every call"}
+    del d16
+
+    # ---- the blst drop-in at 2^20 ----
+    n20 = 1 << 20
+    P20 = (ctypes.c_uint8 * (96 * n20)).from_buffer_copy(bytes(pts)[:96 * n20])
+    k20 = min(K, 10)
+    sets20 = [set_bytes(k, n20) for k in range(k20)]
+    for _ in range(max(W, 1)):
+        dropin(1, P20, sets20[0], n20)
+    r, el = timed(lambda k: dropin(1, P20, sets20[k], n20), k20)
+    legs["blst_p1s_mult_pippenger_2^20"] = {
+        "value": round(n20 * k20 / el, 1), "unit": "pairs/s", "ms_per_step": round(el / k20 * 1e3, 4),
+        "parity_vs_reference": m.compress(1, r[0]).hex() == _golden(m, 1, n20),
+        "note": "the drop-in boundary (pippenger_blst_built_in, main_p1.cpp:400-436): per call 96 MiB of points + "
+                "32 MiB of scalars from pageable host memory, digits/sort overlapping the point upload"}
+    del sets20, P20
+
+    # ---- configs[0]: CPU reference at 2^10, and the drop-in at the same size ----
+    n10 = 1 << 10
+    P10 = (ctypes.c_uint8 * (96 * n10)).from_buffer_copy(bytes(pts)[:96 * n10])
+    S10 = set_bytes(0, n10)
+    want10 = _golden(m, 1, n10)
+    R = _ref_lib("libblst_ref.so")
+    if R is not None:
+        mult = R.blst_p1s_mult_pippenger
+        mult.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+        R.blst_p1s_mult_pippenger_scratch_sizeof.restype = ctypes.c_size_t
+        R.blst_p1s_mult_pippenger_scratch_sizeof.argtypes = [ctypes.c_size_t]
+        scratch = (ctypes.c_uint8 * R.blst_p1s_mult_pippenger_scratch_sizeof(n10))()
+        pp = (ctypes.c_void_p * 2)(ctypes.cast(P10, ctypes.c_void_p), None)
+        spp = (ctypes.c_void_p * 2)(ctypes.cast(S10, ctypes.c_void_p), None)
+        rr = (ctypes.c_uint8 * 144)()
+        reps, t = 0, time.perf_counter()
+        while reps < 5 or time.perf_counter() - t < 0.5:
+            mult(rr, pp, n10, spp, 255, scratch)
+            reps += 1
+        el = time.perf_counter() - t
+        legs["cfg0_cpu_reference_2^10"] = {
+            "value": round(n10 * reps / el, 1), "unit": "pairs/s", "ms_per_step": round(el / reps * 1e3, 4),
+            "cores": 1, "parity_vs_reference": m.compress(1, bytes(rr)).hex() == want10,
+            "note": "configs[0]: the reference's own blst_p1s_mult_pippenger (libblst from /root/reference, "
+                    "oracle/_ref), 1 thread, the pippenger_blst_built_in call of ./run.sh config=10"}
+    for _ in range(3):
+        dropin(1, P10, S10, n10)
+    r, el = timed(lambda k: dropin(1, P10, S10, n10), 20)
+    legs["cfg0_gpu_blst_dropin_2^10"] = {
+        "value": round(n10 * 20 / el, 1), "unit": "pairs/s", "ms_per_step": round(el / 20 * 1e3, 4),
+        "parity_vs_reference": m.compress(1, r[0]).hex() == want10,
+        "note": "the same 2^10 call through the GPU drop-in (launch/latency-bound at this size)"}
+
+    # ---- configs[4]: G2 2^20 CHES batch ----
+    t = time.time()
+    pts2 = m.fixed_points(2, n20)
+    c2 = m.CHESContext(2, local, n_exp=20)
+    c2.build_table(pts2, n20, stream=sp)
+    torch.cuda.synchronize(dev)
+    setup = time.time() - t
+    del pts2
+    k2 = min(K, 10)
+    hptr, SS = host.data_ptr(), 32 * n20
+    d2 = host[:k2 * SS].to(dev)
+    c2.mult_batch(hptr, min(max(W, 1), k2), 32, set_stride=SS, on_device=False, stream=sp)
+    torch.cuda.synchronize(dev)
+    t = time.perf_counter()
+    bh = c2.mult_batch(hptr, k2, 32, set_stride=SS, on_device=False, stream=sp)
+    torch.cuda.synchronize(dev)
+    elh = time.perf_counter() - t
+    acc_h = c2.phase_times()["accumulate"]
+    t = time.perf_counter()
+    br = c2.mult_batch(d2.data_ptr(), k2, 32, set_stride=SS, on_device=True, stream=sp)
+    torch.cuda.synchronize(dev)
+    elr = time.perf_counter() - t
+    sync = [c2.mult(d2.data_ptr() + k * SS, 32, on_device=True, stream=sp) for k in range(2)]
+    c2.set_profiling(True)
+    c2.mult(d2.data_ptr(), 32, on_device=True, stream=sp)
+    ph = c2.phase_times()
+    eq = [m.compress(2, x) for x in bh[:2]] == [m.compress(2, x) for x in sync] and \
+        [m.compress(2, x) for x in br] == [m.compress(2, x) for x in bh]
+    par = c2.params
+    legs["cfg4_g2_ches_batch_h2d"] = {
+        "value": round(n20 * k2 / elh, 1), "unit": "pairs/s", "ms_per_step": round(elh / k2 * 1e3, 4),
+        "kernel_ms": round(acc_h, 4),
+        "valu_frac_alone": round(n20 * par["h"] * 28 / (ph["accumulate"] / 1e3) / FPMUL_PEAK, 4),
+        "phases_ms_sync": {kk: round(v, 4) for kk, v in ph.items()},
+        "parity_vs_reference": m.compress(2, bh[0]).hex() == _golden(m, 2, n20), "batch_equals_sync": eq,
+        "setup_s": round(setup, 2),
+        "note": f"configs[4]: G2 n=2^20 CHES (q=2^{par['q_exp']}, h={par['h']}, |B|={par['b_size']}), table in HBM, "
+                f"{k2} distinct scalar sets in pinned host memory, H2D in the timed region"}
+    legs["cfg4_g2_ches_batch_resident"] = {
+        "value": round(n20 * k2 / elr, 1), "unit": "pairs/s", "ms_per_step": round(elr / k2 * 1e3, 4),
+        "parity_vs_reference": m.compress(2, br[0]).hex() == _golden(m, 2, n20),
+        "note": "configs[4], the same sets resident in HBM"}
+    c2.close()
+    del d2
+    return legs
 
 
 def _ref_lib(name):

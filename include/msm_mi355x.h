@@ -8,8 +8,9 @@
  * MSM entry points below instead of libblst's.  Each declaration cites the
  * reference interface it replaces.
  *
- * Threading: entry points are thread-safe per call (each call uses its own
- * device buffers; engine contexts are not shared across threads unless the
+ * Threading: entry points are thread-safe per call (each blst-named call leases
+ * an engine with its own device buffers and stream from a process-wide pool;
+ * engine contexts are not shared across threads unless the
  * caller serialises).  Errors: the blst-named functions keep blst's void
  * signatures; by default a HIP failure inside one prints the error and aborts
  * (a silent wrong answer is never returned); after msm_set_abort_on_error(0)
@@ -190,6 +191,18 @@ int msm_set_abort_on_error(int on);
 /* nonzero if a blst-named call of this thread failed since the last query (clears it) */
 int msm_error_pending(void);
 int msm_device_count(void);
+/* Engines behind the blst-named entry points (no caller context: ref
+ * multi_scalar.c:581-607) live in a process-wide pool per (device, kind,
+ * window): a call leases one, a concurrent call creates another, and a returned
+ * engine stays cached while the idle engines of its kind on its device hold at
+ * most the cache limit of device memory (default 8 GiB); device memory is thus
+ * bounded by the peak number of concurrent calls, not by the number of calling
+ * threads.  release: frees every idle engine now.  stats: out[0] engines alive
+ * (leased + idle), out[1] idle, out[2] device bytes held by idle engines.
+ * set_limit returns the previous limit. */
+void msm_release_engine_cache(void);
+void msm_engine_cache_stats(size_t out[3]);
+size_t msm_set_engine_cache_limit(size_t bytes);
 /* group 1 (G1) or 2 (G2); points in blst affine layout, host or device memory */
 int msm_ctx_create(msm_ctx **ctx, int group, int device, int window_bits);
 int msm_ctx_set_points(msm_ctx *ctx, const void *points_affine, size_t npoints, int points_on_device,

@@ -30,6 +30,22 @@ def device_count():
     return lib().msm_device_count()
 
 
+def engine_cache_stats():
+    """(engines alive, idle, device bytes of idle engines) of the pool behind the
+    blst-named entry points (include/msm_mi355x.h msm_engine_cache_stats)."""
+    out = (ctypes.c_size_t * 3)()
+    lib().msm_engine_cache_stats(out)
+    return tuple(out)
+
+
+def release_engine_cache():
+    lib().msm_release_engine_cache()
+
+
+def set_engine_cache_limit(nbytes):
+    return lib().msm_set_engine_cache_limit(nbytes)
+
+
 def _buf(data):
     if isinstance(data, (bytes, bytearray)):
         return (ctypes.c_uint8 * len(data)).from_buffer_copy(bytes(data))

@@ -19,6 +19,7 @@
 #include "../../include/msm_mi355x.h"
 #include "engine.hpp"
 #include "multi.hpp"
+#include "pool.hpp"
 
 using namespace msm;
 
@@ -59,41 +60,48 @@ void die(const char *where, const std::exception &e, void *ret = nullptr, size_t
 }
 
 template <int G>
-Pippenger<G> &tls_engine(int window) {
-  thread_local std::map<std::pair<int, int>, std::unique_ptr<Pippenger<G>>> engines;
+std::unique_ptr<typename EnginePool<Pippenger<G>>::Lease> pippenger_engine(int window) {
   int dev = 0;
   MSM_HIP_CHECK(hipGetDevice(&dev));
-  auto key = std::make_pair(dev, window);
-  auto it = engines.find(key);
-  if (it == engines.end()) it = engines.emplace(key, std::make_unique<Pippenger<G>>(dev, window)).first;
-  return *it->second;
+  return EnginePool<Pippenger<G>>::get().lease(dev, window,
+                                               [&] { return std::make_unique<Pippenger<G>>(dev, window); });
 }
 
-// gather the pointer-array inputs into flat host arrays with the reference's
-// iteration rule (ref multi_scalar.c:390-416): the first pointer is always
-// taken; after it, a non-NULL entry names the next element and a NULL entry
-// means "the element right after the previous one" -- so {ptr, NULL} is one
-// flat array and a NULL after k explicit pointers continues contiguously.
-// Scalars advance by nbytes = (nbits+7)/8 (multi_scalar.c:395).
-template <int G>
-void gather(std::vector<uint8_t> &pts, std::vector<uint8_t> &sc, const void *const *points, size_t n,
-            const byte *const *scalars, size_t nbits) {
-  const size_t psz = 96 * G, nb = (nbits + 7) / 8;
-  pts.resize(n * psz);
-  sc.resize(n * nb);
-  if (n == 0) return;
-  const uint8_t *p = (const uint8_t *)*points++;
-  const uint8_t *s = *scalars++;
-  memcpy(pts.data(), p, psz);
-  memcpy(sc.data(), s, nb);
-  for (size_t i = 1; i < n; ++i) {
-    // the reference reads points[i] / scalars[i] only while the previous ones
-    // were non-NULL (multi_scalar.c:413: `*points ? *points++ : point+1`)
-    p = *points ? (const uint8_t *)*points++ : p + psz;
-    s = *scalars ? *scalars++ : s + nb;
-    memcpy(pts.data() + i * psz, p, psz);
-    memcpy(sc.data() + i * nb, s, nb);
+// The n elements of `sz` bytes named by a blst pointer array, with the
+// reference's iteration rule (ref multi_scalar.c:390-416): the first pointer is
+// always taken; after it, a non-NULL entry names the next element and a NULL
+// entry means "the element right after the previous one" -- so {ptr, NULL} is
+// one flat array and a NULL after k explicit pointers continues contiguously.
+// Returns the elements as one contiguous host range: the caller's own memory
+// when they already are one (the flat case; no host copy at all), otherwise a
+// gather into `buf` that copies each run of adjacent elements with one memcpy.
+const uint8_t *contiguous(std::vector<uint8_t> &buf, const void *const *ptrs, size_t n, size_t sz) {
+  if (n == 0) return nullptr;
+  const uint8_t *base = (const uint8_t *)ptrs[0];
+  size_t i = 1;
+  const void *const *pp = ptrs + 1;
+  // walk the explicit pointers while they stay adjacent
+  while (i < n && *pp && (const uint8_t *)*pp == base + i * sz) ++i, ++pp;
+  if (i == n || !*pp) return base;  // all adjacent, or a NULL: the rest continues after the previous element
+  buf.resize(n * sz);
+  memcpy(buf.data(), base, i * sz);
+  const uint8_t *p = base + (i - 1) * sz;
+  while (i < n) {
+    if (!*pp) {  // the rest is contiguous after p
+      memcpy(buf.data() + i * sz, p + sz, (n - i) * sz);
+      break;
+    }
+    const uint8_t *run = (const uint8_t *)*pp++;
+    size_t k = 1;
+    while (i + k < n && *pp && (const uint8_t *)*pp == run + k * sz) ++k, ++pp;
+    if (i + k < n && !*pp) {  // a NULL right after the run extends it to the end
+      k = n - i;
+    }
+    memcpy(buf.data() + i * sz, run, k * sz);
+    p = run + (k - 1) * sz;
+    i += k;
   }
+  return buf.data();
 }
 
 template <int G>
@@ -105,61 +113,43 @@ void mult_pippenger(void *ret, const void *const *points, size_t n, const byte *
     memcpy(ret, &out, sizeof out);
     return;
   }
-  std::vector<uint8_t> pts, sc;
-  gather<G>(pts, sc, points, n, scalars, nbits);
-  Pippenger<G> &eng = tls_engine<G>(auto_window(n));
-  hipStream_t s = 0;
-  eng.set_points(pts.data(), n, false, s);
-  DevBuf dsc;
-  dsc.ensure(sc.size() + 16);
-  MSM_HIP_CHECK(hipMemcpyAsync(dsc.p, sc.data(), sc.size(), hipMemcpyHostToDevice, s));
-  eng.run(s, dsc.as<uint8_t>(), (nbits + 7) / 8, (int)nbits, &out);
+  const size_t nb = (nbits + 7) / 8;
+  std::vector<uint8_t> pbuf, sbuf;
+  const uint8_t *pts = contiguous(pbuf, points, n, 96 * G);
+  const uint8_t *sc = contiguous(sbuf, (const void *const *)scalars, n, nb);
+  auto eng = pippenger_engine<G>(auto_window(n));
+  (*eng)->run_host(eng->stream(), pts, n, sc, nb, (int)nbits, &out);
   memcpy(ret, &out, sizeof out);
 }
 
 // one blst window tile (ref multi_scalar.c:383-419, 587-600): sum_i d_i P_i with
-// d_i the Booth digit of scalar i at [bit0, bit0+wbits) (lookback bit bit0-1).
+// d_i the Booth digit of scalar i at [bit0, bit0+wbits) (lookback bit bit0-1),
+// digits and signs computed on the device (k_tile_booth)
 template <int G>
 void tile_pippenger(void *ret, const void *const *points, size_t n, const byte *const *scalars, size_t nbits,
                     size_t bit0, size_t window) {
   typedef typename HostField<G>::F HF;
-  size_t wbits, cbits;
-  if (bit0 + window > nbits) {
-    wbits = nbits - bit0;
-    cbits = wbits + 1;
-  } else {
-    wbits = cbits = window;
-  }
-  std::vector<uint8_t> pts, sc;
-  gather<G>(pts, sc, points, n, scalars, nbits);
-  const size_t nb = (nbits + 7) / 8, psz = 96 * G;
-  std::vector<uint8_t> small(n * 4, 0);
-  for (size_t i = 0; i < n; ++i) {
-    const uint8_t *s = sc.data() + i * nb;
-    uint32_t v = 0;
-    for (size_t k = 0; k <= wbits; ++k) {  // bits [bit0-1, bit0+wbits)
-      long b = (long)bit0 - 1 + (long)k;
-      if (b < 0 || (size_t)b >= nbits) continue;
-      v |= (uint32_t)((s[b / 8] >> (b % 8)) & 1) << k;
-    }
-    uint32_t sign = (v >> cbits) & 1;
-    int d = (int)((v + 1) >> 1);
-    if (sign) d -= 1 << cbits;
-    if (d < 0) {  // negate the point: y -> p - y
-      d = -d;
-      HF *y = reinterpret_cast<HF *>(pts.data() + i * psz + psz / 2);
-      *y = hfp::neg(*y);
-    }
-    memcpy(small.data() + i * 4, &d, 4);
-  }
-  Pippenger<G> &eng = tls_engine<G>(8);
-  hipStream_t st = 0;
-  eng.set_points(pts.data(), n, false, st);
-  DevBuf dsc;
-  dsc.ensure(small.size() + 16);
-  MSM_HIP_CHECK(hipMemcpyAsync(dsc.p, small.data(), small.size(), hipMemcpyHostToDevice, st));
   hfp::Jac<HF> out;
-  eng.run(st, dsc.as<uint8_t>(), 4, (int)cbits + 1, &out);
+  memset(&out, 0, sizeof out);
+  if (n == 0 || bit0 >= nbits || window == 0 || window > 24) {
+    if (n && (bit0 >= nbits || window == 0 || window > 24)) throw std::runtime_error("tile outside the scalar bits");
+    memcpy(ret, &out, sizeof out);
+    return;
+  }
+  TileSpec t;
+  t.bit0 = (int)bit0;
+  if (bit0 + window > nbits) {
+    t.wbits = (int)(nbits - bit0);
+    t.cbits = t.wbits + 1;
+  } else {
+    t.wbits = t.cbits = (int)window;
+  }
+  const size_t nb = (nbits + 7) / 8;
+  std::vector<uint8_t> pbuf, sbuf;
+  const uint8_t *pts = contiguous(pbuf, points, n, 96 * G);
+  const uint8_t *sc = contiguous(sbuf, (const void *const *)scalars, n, nb);
+  auto eng = pippenger_engine<G>(8);
+  (*eng)->run_host(eng->stream(), pts, n, sc, nb, (int)nbits, &out, &t);
   memcpy(ret, &out, sizeof out);
 }
 
@@ -251,32 +241,23 @@ void tile_bgmw95(void *ret, const void *const *points, size_t n, const int *scal
 // (one lane accumulates each bucket), then the weighted reduction sums them
 template <int G>
 void points_add(void *ret, const void *const *points, size_t n) {
-  const size_t psz = 96 * G;
-  std::vector<uint8_t> flat(n * psz);
-  const uint8_t *pt = nullptr;
-  for (size_t i = 0; i < n; ++i) {
-    pt = *points ? (const uint8_t *)*points++ : pt + psz;
-    memcpy(flat.data() + i * psz, pt, psz);
-  }
+  std::vector<uint8_t> buf;
+  const uint8_t *flat = contiguous(buf, points, n, 96 * G);
   const size_t nb = std::max<size_t>(1, std::min<size_t>(n, 4096));
   std::vector<uint32_t> keys(n), vals(n), w(nb, 1);
   for (size_t i = 0; i < n; ++i) {
     keys[i] = (uint32_t)(i % nb);
     vals[i] = (uint32_t)i;
   }
-  entry_msm<G>(ret, flat.data(), n, keys.data(), vals.data(), n, nb, w.data(), nullptr);
+  entry_msm<G>(ret, flat, n, keys.data(), vals.data(), n, nb, w.data(), nullptr);
 }
 
 // ---- fixed-window MSM with a precomputed table (ref multi_scalar.c:63-261) ----
 template <int G>
-Wbits<G> &tls_wbits(int wbits) {
-  thread_local std::map<std::pair<int, int>, std::unique_ptr<Wbits<G>>> engines;
+std::unique_ptr<typename EnginePool<Wbits<G>>::Lease> wbits_engine(int wbits) {
   int dev = 0;
   MSM_HIP_CHECK(hipGetDevice(&dev));
-  auto key = std::make_pair(dev, wbits);
-  auto it = engines.find(key);
-  if (it == engines.end()) it = engines.emplace(key, std::make_unique<Wbits<G>>(dev, wbits)).first;
-  return *it->second;
+  return EnginePool<Wbits<G>>::get().lease(dev, wbits, [&] { return std::make_unique<Wbits<G>>(dev, wbits); });
 }
 
 // all points are read (pointer rule of ref multi_scalar.c:136: a NULL entry
@@ -284,17 +265,12 @@ Wbits<G> &tls_wbits(int wbits) {
 // binding's in-place call (points at the end of the table, blst.hpp:383-393) works
 template <int G>
 void wbits_precompute(void *table, size_t wbits, const void *const *points, size_t n) {
-  const size_t psz = 96 * G;
-  std::vector<uint8_t> flat(n * psz);
-  const uint8_t *pt = nullptr;
-  for (size_t i = 0; i < n; ++i) {
-    pt = *points ? (const uint8_t *)*points++ : pt + psz;
-    memcpy(flat.data() + i * psz, pt, psz);
-  }
   if (!n) return;
-  Wbits<G> &eng = tls_wbits<G>((int)wbits);
-  eng.precompute(flat.data(), n, false, (hipStream_t)0);
-  eng.get_table(table, 0, eng.table_rows(), (hipStream_t)0);
+  std::vector<uint8_t> buf;
+  const uint8_t *flat = contiguous(buf, points, n, 96 * G);
+  auto eng = wbits_engine<G>((int)wbits);
+  (*eng)->precompute(flat, n, false, eng->stream());
+  (*eng)->get_table(table, 0, (*eng)->table_rows(), eng->stream());
 }
 
 // scalar pointer rule of ref multi_scalar.c:165,191: the first pointer is
@@ -306,19 +282,13 @@ void wbits_mult(void *ret, const void *table, size_t wbits, size_t n, const byte
   memset(&out, 0, sizeof out);
   if (n && nbits) {
     const size_t nb = (nbits + 7) / 8;
-    std::vector<uint8_t> sc(n * nb);
-    const uint8_t *s = *scalars++;
-    memcpy(sc.data(), s, nb);
-    for (size_t i = 1; i < n; ++i) {
-      s = *scalars ? *scalars++ : s + nb;
-      memcpy(sc.data() + i * nb, s, nb);
-    }
-    Wbits<G> &eng = tls_wbits<G>((int)wbits);
-    eng.set_table(table, n, false, (hipStream_t)0);
-    DevBuf d;
-    d.ensure(sc.size() + 16);
-    MSM_HIP_CHECK(hipMemcpy(d.p, sc.data(), sc.size(), hipMemcpyHostToDevice));
-    eng.run((hipStream_t)0, d.as<uint8_t>(), nb, (int)nbits, &out);
+    std::vector<uint8_t> buf;
+    const uint8_t *sc = contiguous(buf, (const void *const *)scalars, n, nb);
+    auto eng = wbits_engine<G>((int)wbits);
+    hipStream_t s = eng->stream();
+    (*eng)->set_table(table, n, false, s);
+    (*eng)->upload_scalars(sc, n * nb, s);
+    (*eng)->run(s, nullptr, nb, (int)nbits, &out);
   }
   memcpy(ret, &out, sizeof out);
 }
@@ -658,6 +628,24 @@ int msm_error_pending(void) {
   const int p = g_pending;
   g_pending = 0;
   return p;
+}
+
+void msm_release_engine_cache(void) {
+  PoolStats st;
+  PoolRegistry::get().visit(st, true);
+}
+
+void msm_engine_cache_stats(size_t out[3]) {
+  PoolStats st;
+  PoolRegistry::get().visit(st, false);
+  out[0] = st.live, out[1] = st.idle, out[2] = st.idle_bytes;
+}
+
+size_t msm_set_engine_cache_limit(size_t bytes) {
+  std::lock_guard<std::mutex> g(PoolRegistry::get().mu);
+  const size_t prev = PoolRegistry::get().idle_budget;
+  PoolRegistry::get().idle_budget = bytes;
+  return prev;
 }
 
 int msm_device_count(void) {

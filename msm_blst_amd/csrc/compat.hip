@@ -17,6 +17,7 @@
 #include "ches_kernels.hpp"
 #include "engine.hpp"
 #include "pair_kernels.hpp"
+#include "pool.hpp"
 
 #ifndef MSM_GROUP
 #error "define MSM_GROUP (1 or 2)"
@@ -30,16 +31,19 @@ struct EntryMsmState {
   BucketSort sort;
   WeightedReducer<G> red;
   std::vector<uint32_t> planned;  // weights the reducer plan was built for
+  size_t device_bytes() const {
+    size_t b = 0;
+    for (const DevBuf *d : {&pts, &keys, &vals, &sorted, &counts, &offsets, &order, &buckets, &xfer, &bx}) b += d->bytes;
+    return b;
+  }
 };
 
+// pooled per device (pool.hpp): concurrent tile calls each lease their own state
 template <int G>
-static EntryMsmState<G> &entry_state() {
-  thread_local std::map<int, std::unique_ptr<EntryMsmState<G>>> st;
+static std::unique_ptr<typename EnginePool<EntryMsmState<G>>::Lease> entry_state() {
   int dev = 0;
   MSM_HIP_CHECK(hipGetDevice(&dev));
-  auto &p = st[dev];
-  if (!p) p = std::make_unique<EntryMsmState<G>>();
-  return *p;
+  return EnginePool<EntryMsmState<G>>::get().lease(dev, 0, [] { return std::make_unique<EntryMsmState<G>>(); });
 }
 
 template <int G>
@@ -54,14 +58,15 @@ void entry_msm(void *ret, const void *pts_blst, size_t npts, const uint32_t *key
                size_t nb, const uint32_t *weights, void *buckets_out) {
   typedef typename FieldOf<G>::F F;
   typedef typename HostField<G>::F HF;
-  EntryMsmState<G> &S = entry_state<G>();
-  hipStream_t s = 0;
   hfp::Jac<HF> out;
   std::memset(&out, 0, sizeof out);
   if (nb == 0) {
     std::memcpy(ret, &out, sizeof out);
     return;
   }
+  auto lease = entry_state<G>();
+  EntryMsmState<G> &S = **lease;
+  hipStream_t s = lease->stream();
   if (ne >= (1ull << 31) || npts >= (1ull << 31)) throw std::runtime_error("entry MSM too large");
   S.xfer.ensure(std::max<size_t>(npts * 96 * G, 16));
   S.pts.ensure(std::max<size_t>(npts, 1) * sizeof(Aff<F>));
@@ -106,14 +111,15 @@ template <int G>
 void weighted_bucket_sum(void *ret, const void *buckets_blst, size_t nb, const uint32_t *weights) {
   typedef typename FieldOf<G>::F F;
   typedef typename HostField<G>::F HF;
-  EntryMsmState<G> &S = entry_state<G>();
-  hipStream_t s = 0;
   hfp::Jac<HF> out;
   std::memset(&out, 0, sizeof out);
   if (nb == 0) {
     std::memcpy(ret, &out, sizeof out);
     return;
   }
+  auto lease = entry_state<G>();
+  EntryMsmState<G> &S = **lease;
+  hipStream_t s = lease->stream();
   S.xfer.ensure(nb * 192 * G);
   S.buckets.ensure(nb * sizeof(Xyzz<F>));
   MSM_HIP_CHECK(hipMemcpyAsync(S.xfer.p, buckets_blst, nb * 192 * G, hipMemcpyHostToDevice, s));

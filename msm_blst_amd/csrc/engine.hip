@@ -66,6 +66,12 @@ Pippenger<G>::Pippenger(int device, int window_bits) : dev_(device), c_(window_b
 template <int G>
 Pippenger<G>::~Pippenger() {
   for (auto &e : ev_) (void)hipEventDestroy(e);
+  if (up_) {
+    (void)hipStreamSynchronize(up_);
+    (void)hipStreamDestroy(up_);
+    (void)hipEventDestroy(ev_up_);
+    (void)hipEventDestroy(ev_s_);
+  }
 }
 
 template <int G>
@@ -93,8 +99,8 @@ void Pippenger<G>::set_points(const void *pts, size_t n, bool on_device, hipStre
 
 template <int C>
 static void launch_digits(hipStream_t s, const uint8_t *sc, size_t stride, size_t n, int nbits, int W, uint32_t *keys,
-                          uint32_t *vals) {
-  hipLaunchKernelGGL(k_digits<C>, dim3(nblk(n, 256)), dim3(256), 0, s, sc, stride, n, nbits, W, keys, vals);
+                          uint32_t *vals, const uint8_t *neg) {
+  hipLaunchKernelGGL(k_digits<C>, dim3(nblk(n, 256)), dim3(256), 0, s, sc, stride, n, nbits, W, keys, vals, neg);
 }
 
 #define MSM_C_DISPATCH(c, FN, ...)                          \
@@ -112,22 +118,11 @@ static void launch_digits(hipStream_t s, const uint8_t *sc, size_t stride, size_
   }
 
 template <int G>
-void Pippenger<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, int nbits, hfp::Jac<HF> *out) {
-  typedef typename FieldOf<G>::F F;
-  DeviceGuard g(dev_);
-  if (nbits < 1 || nbits > 256) throw std::runtime_error("nbits must be in [1,256]");
+void Pippenger<G>::front(hipStream_t s, const uint8_t *d_scalars, size_t stride, int nbits, const uint8_t *neg) {
   const int c = c_;
   const int W = (nbits + 1 + c - 1) / c;
   const size_t NB = (size_t)1 << (c - 1);
   const size_t NT = (size_t)W * NB;
-  hfp::Jac<HF> ret;
-  ret.x = hfp::fzero(HF());
-  ret.y = hfp::fzero(HF());
-  ret.z = hfp::fzero(HF());
-  if (n_ == 0) {
-    *out = ret;
-    return;
-  }
   const size_t n = n_, ne = (size_t)W * n;
   keys_.ensure(ne * 4);
   vals_.ensure(ne * 4);
@@ -135,15 +130,23 @@ void Pippenger<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, i
   counts_.ensure(NT * 4);
   offsets_.ensure(NT * 4);
   order_.ensure(NT * 4);
-  buckets_.ensure(NT * sizeof(Xyzz<F>));
-
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[0], s));
-  MSM_C_DISPATCH(c, launch_digits, s, d_scalars, stride, n, nbits, W, keys_.as<uint32_t>(), vals_.as<uint32_t>());
+  MSM_C_DISPATCH(c, launch_digits, s, d_scalars, stride, n, nbits, W, keys_.as<uint32_t>(), vals_.as<uint32_t>(), neg);
   MSM_HIP_CHECK(hipGetLastError());
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[1], s));
   sort_.run(s, keys_.as<uint32_t>(), vals_.as<uint32_t>(), ne, (uint32_t)NT, sorted_.as<uint32_t>(),
             counts_.as<uint32_t>(), offsets_.as<uint32_t>(), order_.as<uint32_t>());
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[2], s));
+}
+
+template <int G>
+void Pippenger<G>::back(hipStream_t s, int nbits, hfp::Jac<HF> *out) {
+  typedef typename FieldOf<G>::F F;
+  const int c = c_;
+  const int W = (nbits + 1 + c - 1) / c;
+  const size_t NB = (size_t)1 << (c - 1);
+  const size_t NT = (size_t)W * NB;
+  buckets_.ensure(NT * sizeof(Xyzz<F>));
   launch_accumulate<G>(s, order_.as<uint32_t>(), counts_.as<uint32_t>(), offsets_.as<uint32_t>(),
                        sorted_.as<uint32_t>(), pts_.as<Aff<F>>(), buckets_.as<Xyzz<F>>(), NT);
   MSM_HIP_CHECK(hipGetLastError());
@@ -176,6 +179,71 @@ void Pippenger<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, i
     times_.total = ms;
     times_.accumulate_launches = 1;
   }
+}
+
+template <int G>
+void Pippenger<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, int nbits, hfp::Jac<HF> *out) {
+  DeviceGuard g(dev_);
+  if (nbits < 1 || nbits > 256) throw std::runtime_error("nbits must be in [1,256]");
+  if (n_ == 0) {
+    *out = hfp::Jac<HF>{hfp::fzero(HF()), hfp::fzero(HF()), hfp::fzero(HF())};
+    return;
+  }
+  front(s, d_scalars, stride, nbits, nullptr);
+  back(s, nbits, out);
+}
+
+// The blst drop-in (abi.cpp blst_p{1,2}s_mult_pippenger / _tile_pippenger):
+// points and scalars in the caller's host memory.  The scalars go up first and
+// their digits + sort are enqueued; the 96 n G bytes of points then upload (and
+// convert) on a second stream while the GPU sorts, and the accumulation waits
+// for them.  tile != nullptr: one blst window tile -- k_tile_booth turns the
+// raw scalars into |Booth digit| + sign on the device, and the plain pipeline
+// multiplies with |d| (cbits + 1 bits) and the signs.
+template <int G>
+void Pippenger<G>::run_host(hipStream_t s, const void *pts_blst, size_t n, const uint8_t *scalars, size_t stride,
+                            int nbits, hfp::Jac<HF> *out, const TileSpec *tile) {
+  typedef typename FieldOf<G>::F F;
+  DeviceGuard g(dev_);
+  if (nbits < 1 || nbits > 256) throw std::runtime_error("nbits must be in [1,256]");
+  if (n >= (1ull << 31)) throw std::runtime_error("too many points");
+  n_ = n;
+  if (n == 0) {
+    *out = hfp::Jac<HF>{hfp::fzero(HF()), hfp::fzero(HF()), hfp::fzero(HF())};
+    return;
+  }
+  if (!up_) {
+    MSM_HIP_CHECK(hipStreamCreateWithFlags(&up_, hipStreamNonBlocking));
+    MSM_HIP_CHECK(hipEventCreateWithFlags(&ev_up_, hipEventDisableTiming));
+    MSM_HIP_CHECK(hipEventCreateWithFlags(&ev_s_, hipEventDisableTiming));
+  }
+  const size_t sbytes = n * stride;
+  scal_.ensure(sbytes + (tile ? n * 5 : 0) + 16);
+  MSM_HIP_CHECK(hipMemcpyAsync(scal_.p, scalars, sbytes, hipMemcpyHostToDevice, s));
+  if (tile) {
+    uint32_t *mag = reinterpret_cast<uint32_t *>(scal_.as<uint8_t>() + ((sbytes + 3) & ~(size_t)3));
+    uint8_t *neg = reinterpret_cast<uint8_t *>(mag + n);
+    hipLaunchKernelGGL(k_tile_booth, dim3(nblk(n, 256)), dim3(256), 0, s, scal_.as<uint8_t>(), stride, n, nbits,
+                       tile->bit0, tile->wbits, tile->cbits, mag, neg);
+    MSM_HIP_CHECK(hipGetLastError());
+    nbits = tile->cbits + 1;
+    front(s, reinterpret_cast<const uint8_t *>(mag), 4, nbits, neg);
+  } else {
+    front(s, scal_.as<uint8_t>(), stride, nbits, nullptr);
+  }
+  // the upload stream must not overwrite points an earlier MSM on s still reads
+  MSM_HIP_CHECK(hipEventRecord(ev_s_, s));
+  MSM_HIP_CHECK(hipStreamWaitEvent(up_, ev_s_, 0));
+  const size_t raw = n * 96 * G;
+  tmp_.ensure(raw);
+  pts_.ensure(n * sizeof(Aff<F>));
+  MSM_HIP_CHECK(hipMemcpyAsync(tmp_.p, pts_blst, raw, hipMemcpyHostToDevice, up_));
+  hipLaunchKernelGGL(k_convert_points<G>, dim3(nblk(n, 256)), dim3(256), 0, up_, tmp_.as<uint64_t>(),
+                     pts_.as<Aff<F>>(), n);
+  MSM_HIP_CHECK(hipGetLastError());
+  MSM_HIP_CHECK(hipEventRecord(ev_up_, up_));
+  MSM_HIP_CHECK(hipStreamWaitEvent(s, ev_up_, 0));
+  back(s, nbits, out);
 }
 
 template <int G>

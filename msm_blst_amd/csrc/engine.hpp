@@ -194,6 +194,12 @@ class WeightedReducer {
   DevBuf bfin_;
 };
 
+// one blst window tile (ref multi_scalar.c:383-419): Booth digit over bits
+// [bit0 - 1, bit0 + wbits), cbits = wbits (+ 1 for the top, partial window)
+struct TileSpec {
+  int bit0, wbits, cbits;
+};
+
 // Plain Pippenger bucket method (ref src/multi_scalar.c:549-576) on one GPU.
 template <int G>
 class Pippenger {
@@ -205,18 +211,34 @@ class Pippenger {
   void set_points(const void *points_blst, size_t n, bool on_device, hipStream_t s);
   // scalars: n little-endian byte strings with the given stride, on device
   void run(hipStream_t s, const uint8_t *d_scalars, size_t stride, int nbits, hfp::Jac<HF> *out);
+  // points (blst affine) and scalars in host memory: set_points + run with the
+  // point upload overlapping the scalars' digits and sort (blst drop-in)
+  // tile: one blst window tile instead of the whole MSM (blst_p{1,2}s_tile_pippenger)
+  void run_host(hipStream_t s, const void *points_blst, size_t n, const uint8_t *scalars, size_t stride, int nbits,
+                hfp::Jac<HF> *out, const TileSpec *tile = nullptr);
   size_t npoints() const { return n_; }
   void set_profiling(bool on) { profile_ = on; }
   const PhaseTimes &times() const { return times_; }
   int device() const { return dev_; }
   int window_bits() const { return c_; }
+  size_t device_bytes() const {
+    size_t b = 0;
+    for (const DevBuf *d : {&pts_, &keys_, &vals_, &counts_, &offsets_, &sorted_, &order_, &buckets_, &tmp_, &scal_})
+      b += d->bytes;
+    return b;
+  }
 
  private:
   int dev_, c_;
   size_t n_ = 0;
   bool profile_ = false;
   PhaseTimes times_;
-  DevBuf pts_, keys_, vals_, counts_, offsets_, sorted_, order_, buckets_, tmp_;
+  DevBuf pts_, keys_, vals_, counts_, offsets_, sorted_, order_, buckets_, tmp_, scal_;
+  hipStream_t up_ = nullptr;  // run_host: point upload stream
+  hipEvent_t ev_up_ = nullptr, ev_s_ = nullptr;
+  // digits + sort; neg: optional per-point sign flips (tiles)
+  void front(hipStream_t s, const uint8_t *d_scalars, size_t stride, int nbits, const uint8_t *neg);
+  void back(hipStream_t s, int nbits, hfp::Jac<HF> *out);  // accumulate + reduce + read-back
   BucketSort sort_;
   WeightedReducer<G> red_;
   int red_W_ = 0;  // window count the reducer plan was built for
@@ -250,10 +272,10 @@ class Ches {
   void run(hipStream_t s, const uint8_t *d_scalars, size_t stride, hfp::Jac<HF> *out);
   // `count` MSMs over the same points; scalar set k at scalars + k * set_stride,
   // in device memory or (scalars_on_host) host memory -- then each set is copied
-  // into one of kFronts device slots right before its digit conversion, on the
-  // front stream, overlapping earlier MSMs' accumulations (pinned host memory
-  // for a truly asynchronous copy).  Pipelined: MSM k's reduction runs on a
-  // second stream beside MSM k+1's accumulation.
+  // into one of kSlots device slots on its own copy stream (cstream_), ahead of
+  // its digit conversion and overlapping earlier MSMs' accumulations (pinned
+  // host memory for a truly asynchronous copy).  Pipelined: MSM k's reduction
+  // runs on a second stream beside MSM k+1's accumulation.
   void run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, size_t set_stride, size_t count,
                  hfp::Jac<HF> *outs, bool scalars_on_host = false);
   size_t npoints() const { return n_; }
@@ -352,17 +374,20 @@ class Wbits {
   // a table in the reference layout (blst affine, n << (wbits-1) rows), host or device
   void set_table(const void *table_blst, size_t n, bool on_device, hipStream_t s);
   void get_table(void *out_blst, size_t first, size_t count, hipStream_t s);
-  // scalars: n little-endian strings of `stride` bytes on device; low nbits bits used
+  // scalars: n little-endian strings of `stride` bytes on device (nullptr: the
+  // set last given to upload_scalars); low nbits bits used
   void run(hipStream_t s, const uint8_t *d_scalars, size_t stride, int nbits, hfp::Jac<HF> *out);
+  void upload_scalars(const void *host, size_t bytes, hipStream_t s);
   size_t npoints() const { return n_; }
   size_t table_rows() const { return n_ << (wbits_ - 1); }
   int wbits() const { return wbits_; }
   int device() const { return dev_; }
+  size_t device_bytes() const { return table_.bytes + parts_[0].bytes + parts_[1].bytes + fin_.bytes + scal_.bytes; }
 
  private:
   int dev_, wbits_;
   size_t n_ = 0;
-  DevBuf table_, parts_[2], fin_;
+  DevBuf table_, parts_[2], fin_, scal_;
 };
 
 // blst-level tile entry points (compat.hip): sum_b weights[b] * (sum of the

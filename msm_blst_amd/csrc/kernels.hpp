@@ -162,11 +162,13 @@ __device__ __forceinline__ uint32_t scalar_bits(const uint32_t s[10], int off, i
   return (uint32_t)(v >> sh) & ((1u << c) - 1u);
 }
 
+// neg (optional): entry i's point enters negated (blst tile digits, k_tile_booth)
 template <int C>
 __global__ void k_digits(const uint8_t *__restrict__ scalars, size_t stride, size_t n, int nbits, int W,
-                         uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+                         uint32_t *__restrict__ keys, uint32_t *__restrict__ vals, const uint8_t *__restrict__ neg) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  const uint32_t flip = neg ? (uint32_t)(neg[i] != 0) : 0u;
   constexpr uint32_t NB = 1u << (C - 1);
   const uint8_t *sp = scalars + i * stride;
   int nbytes = (nbits + 7) / 8;
@@ -208,12 +210,34 @@ __global__ void k_digits(const uint8_t *__restrict__ scalars, size_t stride, siz
       size_t e = (size_t)w * n + i;
       if (b) {
         keys[e] = (uint32_t)w * NB + (b - 1);
-        vals[e] = (uint32_t)i | (sign << 31);
+        vals[e] = (uint32_t)i | ((sign ^ flip) << 31);
       } else {
         keys[e] = KEY_NONE;
       }
     }
   }
+}
+
+// One blst window tile (ref multi_scalar.c:383-419 with ec_mult.h:23-55): the
+// Booth digit of scalar i over bits [bit0 - 1, bit0 + wbits) (lookback bit
+// bit0 - 1; bits >= nbits read as 0), split into |d| (a 4-byte "scalar" the
+// plain pipeline multiplies with) and the sign (neg[i], applied by k_digits).
+static __global__ void k_tile_booth(const uint8_t *__restrict__ scalars, size_t stride, size_t n, int nbits, int bit0,
+                             int wbits, int cbits, uint32_t *__restrict__ mag, uint8_t *__restrict__ neg) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t *sp = scalars + i * stride;
+  uint32_t v = 0;
+  for (int k = 0; k <= wbits; ++k) {
+    const int b = bit0 - 1 + k;
+    if (b < 0 || b >= nbits) continue;
+    v |= (uint32_t)((sp[b >> 3] >> (b & 7)) & 1) << k;
+  }
+  const uint32_t sign = (v >> cbits) & 1;
+  int d = (int)((v + 1) >> 1);
+  if (sign) d -= 1 << cbits;
+  mag[i] = (uint32_t)(d < 0 ? -d : d);
+  neg[i] = (uint8_t)(d < 0);
 }
 
 static __global__ void k_iota(uint32_t *a, size_t n) {

@@ -241,6 +241,7 @@ void Wbits<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, int n
   std::memset(out, 0, sizeof(*out));
   if (n_ == 0 || nbits <= 0) return;
   if ((size_t)(nbits + 7) / 8 > stride) throw std::runtime_error("scalar stride shorter than nbits");
+  if (!d_scalars) d_scalars = scal_.as<uint8_t>();  // upload_scalars()
   const int nw = nbits / wbits_ + 1;  // windows 0..K, K = floor(nbits / wbits) (ref multi_scalar.c:174-227)
   // chunk of points per lane: ~2^17 lanes in flight
   const size_t C = std::max<size_t>(1, (n_ * (size_t)nw + ((size_t)1 << 17) - 1) >> 17);
@@ -267,6 +268,13 @@ void Wbits<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, int n
   MSM_HIP_CHECK(hipMemcpyAsync(T.data(), fin_.p, (size_t)nw * sizeof(hfp::Jac<HF>), hipMemcpyDeviceToHost, s));
   MSM_HIP_CHECK(hipStreamSynchronize(s));
   *out = horner(T, wbits_);  // sum_w 2^(wbits w) T_w
+}
+
+template <int G>
+void Wbits<G>::upload_scalars(const void *host, size_t bytes, hipStream_t s) {
+  DeviceGuard g(dev_);
+  scal_.ensure(bytes + 16);
+  MSM_HIP_CHECK(hipMemcpyAsync(scal_.p, host, bytes, hipMemcpyHostToDevice, s));
 }
 
 template class Wbits<MSM_GROUP>;

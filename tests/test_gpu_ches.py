@@ -144,14 +144,19 @@ def test_mult_batch_matches_single(m, golden):
     ctx.close()
 
 
-@pytest.mark.parametrize("group,log_n", [(1, 16), (2, 10)])
-def test_mult_batch_sets_resident_and_pinned(m, group, log_n):
-    """Batches longer than every ring (3 front sets, 3 bucket sets, 3 scalar
-    slots): 7 distinct sets from device memory and from page-locked host memory
-    (streamed set by set inside the pipeline) equal the synchronous MSMs."""
+@pytest.mark.parametrize("group,log_n,K", [(1, 16, 7), (2, 10, 7), (1, 12, 9), (1, 12, 17), (2, 10, 9),
+                                           (2, 10, 17)])
+def test_mult_batch_sets_resident_and_pinned(m, group, log_n, K):
+    """Batches longer than every ring (Ches: kFronts = 3 front sets, kBSets = 2
+    bucket sets, kSlots = 4 device scalar slots whose copies run on their own
+    copy stream): K distinct sets from device memory and from page-locked host
+    memory (streamed set by set inside the pipeline) equal the synchronous MSMs.
+    K = 9 and 17 exceed one reduction group (kGroup = 8): several groups of
+    uneven size R alternate between the two reducer buffer sets / tail streams
+    and read back at their own offsets."""
     import numpy as np
     import torch
-    n, K = 1 << log_n, 7
+    n = 1 << log_n
     ctx = m.CHESContext(group, 0, n_exp=log_n)
     ctx.build_table(m.fixed_points(group, n), n)
     host = torch.empty(K * n * 32, dtype=torch.uint8, pin_memory=True)
