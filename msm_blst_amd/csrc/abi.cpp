@@ -31,15 +31,20 @@ int fail(int code, const std::string &msg) {
   return code;
 }
 
+// window of the blst drop-in's plain Pippenger: the fastest c measured on
+// MI355X per n (tools/window_sweep.py, profiles/r03_window_sweep.json; blst's
+// own rule, multi_scalar.c:268-275, picks smaller windows: CPU buckets are
+// cache-bound, GPU lanes want enough buckets to fill the chip)
 int auto_window(size_t n) {
   int lg = 0;
   while (((size_t)1 << (lg + 1)) <= n) ++lg;
-  int c = lg - 4;
-  if (c < 8) c = 8;
-  if (c > 16) c = 16;
-  if (c == 9) c = 10;
-  if (c == 11) c = 12;
-  return c;
+  if (lg <= 8) return 8;
+  if (lg <= 10) return 10;
+  if (lg <= 12) return 12;
+  if (lg == 13) return 13;
+  if (lg <= 16) return 14;
+  if (lg <= 21) return 16;
+  return 17;
 }
 
 // Failure inside a void blst-named entry point.  Default: print and abort (a
@@ -131,11 +136,13 @@ void tile_pippenger(void *ret, const void *const *points, size_t n, const byte *
   typedef typename HostField<G>::F HF;
   hfp::Jac<HF> out;
   memset(&out, 0, sizeof out);
-  if (n == 0 || bit0 >= nbits || window == 0 || window > 24) {
-    if (n && (bit0 >= nbits || window == 0 || window > 24)) throw std::runtime_error("tile outside the scalar bits");
+  // bit0 == nbits is legal: the top tile of nbits = 256 with 8-bit windows holds
+  // only the Booth carry of bit 255 (wbits = 0, cbits = 1; ref multi_scalar.c:596-599)
+  if (n == 0) {
     memcpy(ret, &out, sizeof out);
     return;
   }
+  if (bit0 > nbits || window == 0 || window > 24) throw std::runtime_error("tile outside the scalar bits");
   TileSpec t;
   t.bit0 = (int)bit0;
   if (bit0 + window > nbits) {

@@ -99,8 +99,8 @@ void Pippenger<G>::set_points(const void *pts, size_t n, bool on_device, hipStre
 
 template <int C>
 static void launch_digits(hipStream_t s, const uint8_t *sc, size_t stride, size_t n, int nbits, int W, uint32_t *keys,
-                          uint32_t *vals, const uint8_t *neg) {
-  hipLaunchKernelGGL(k_digits<C>, dim3(nblk(n, 256)), dim3(256), 0, s, sc, stride, n, nbits, W, keys, vals, neg);
+                          uint32_t *vals, const uint8_t *neg, int tcl) {
+  hipLaunchKernelGGL(k_digits<C>, dim3(nblk(n, 256)), dim3(256), 0, s, sc, stride, n, nbits, W, keys, vals, neg, tcl);
 }
 
 #define MSM_C_DISPATCH(c, FN, ...)                          \
@@ -131,7 +131,8 @@ void Pippenger<G>::front(hipStream_t s, const uint8_t *d_scalars, size_t stride,
   offsets_.ensure(NT * 4);
   order_.ensure(NT * 4);
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[0], s));
-  MSM_C_DISPATCH(c, launch_digits, s, d_scalars, stride, n, nbits, W, keys_.as<uint32_t>(), vals_.as<uint32_t>(), neg);
+  MSM_C_DISPATCH(c, launch_digits, s, d_scalars, stride, n, nbits, W, keys_.as<uint32_t>(), vals_.as<uint32_t>(), neg,
+                 top_copies_log2(nbits));
   MSM_HIP_CHECK(hipGetLastError());
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[1], s));
   sort_.run(s, keys_.as<uint32_t>(), vals_.as<uint32_t>(), ne, (uint32_t)NT, sorted_.as<uint32_t>(),
@@ -151,11 +152,18 @@ void Pippenger<G>::back(hipStream_t s, int nbits, hfp::Jac<HF> *out) {
                        sorted_.as<uint32_t>(), pts_.as<Aff<F>>(), buckets_.as<Xyzz<F>>(), NT);
   MSM_HIP_CHECK(hipGetLastError());
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[3], s));
-  if (red_W_ != W) {  // bucket (w, b-1) has weight b in window w; plan once per window layout
+  const int tcl = top_copies_log2(nbits);
+  if (red_W_ != W || red_tcl_ != tcl) {  // bucket (w, b-1) has weight b in window w; plan once per layout
     std::vector<uint32_t> wt(NT), win(NT);
-    for (size_t k = 0; k < NT; ++k) wt[k] = (uint32_t)(k % NB) + 1, win[k] = (uint32_t)(k / NB);
+    const size_t ntop = NB >> tcl;  // top window: slot k holds a copy of bucket (k mod ntop) + 1
+    for (size_t k = 0; k < NT; ++k) {
+      const size_t w = k / NB, b = k % NB;
+      wt[k] = (uint32_t)((w == (size_t)W - 1 ? b % ntop : b) + 1);
+      win[k] = (uint32_t)w;
+    }
     red_.plan(wt, win, W);
     red_W_ = W;
+    red_tcl_ = tcl;
   }
   red_.launch(s, buckets_.p);
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[4], s));

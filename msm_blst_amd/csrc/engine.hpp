@@ -241,7 +241,14 @@ class Pippenger {
   void back(hipStream_t s, int nbits, hfp::Jac<HF> *out);  // accumulate + reduce + read-back
   BucketSort sort_;
   WeightedReducer<G> red_;
-  int red_W_ = 0;  // window count the reducer plan was built for
+  int red_W_ = 0, red_tcl_ = -1;  // window count / top copies the reducer plan was built for
+  // log2 of the top window's bucket copies (k_digits): 2^topbits digit values
+  // spread over its 2^(c-1) slots
+  int top_copies_log2(int nbits) const {
+    const int W = (nbits + 1 + c_ - 1) / c_;
+    const int topbits = nbits - (W - 1) * c_;  // in [0, c - 1]
+    return c_ - 1 - topbits;
+  }
   std::vector<hipEvent_t> ev_;
 };
 

@@ -163,9 +163,15 @@ __device__ __forceinline__ uint32_t scalar_bits(const uint32_t s[10], int off, i
 }
 
 // neg (optional): entry i's point enters negated (blst tile digits, k_tile_booth)
+// Top window: its digits take only 2^topbits values (topbits = nbits - (W-1) C
+// <= C - 1; e.g. 3 for C = 12, nbits = 255), so one lane per bucket would run
+// n / 2^topbits sequential madds there.  Its NB slots instead hold 2^tcl copies
+// of its 2^topbits buckets (entry i -> copy i mod 2^tcl), each copy weighted
+// like its bucket in the reduction plan (Pippenger<G>::back).
 template <int C>
 __global__ void k_digits(const uint8_t *__restrict__ scalars, size_t stride, size_t n, int nbits, int W,
-                         uint32_t *__restrict__ keys, uint32_t *__restrict__ vals, const uint8_t *__restrict__ neg) {
+                         uint32_t *__restrict__ keys, uint32_t *__restrict__ vals, const uint8_t *__restrict__ neg,
+                         int tcl) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t flip = neg ? (uint32_t)(neg[i] != 0) : 0u;
@@ -209,7 +215,8 @@ __global__ void k_digits(const uint8_t *__restrict__ scalars, size_t stride, siz
       }
       size_t e = (size_t)w * n + i;
       if (b) {
-        keys[e] = (uint32_t)w * NB + (b - 1);
+        const uint32_t copy = w == W - 1 ? ((uint32_t)i & ((1u << tcl) - 1u)) << (C - 1 - tcl) : 0u;
+        keys[e] = (uint32_t)w * NB + (b - 1) + copy;
         vals[e] = (uint32_t)i | ((sign ^ flip) << 31);
       } else {
         keys[e] = KEY_NONE;
