@@ -13,14 +13,18 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
-OBJ = os.path.join(HERE, "_build")
-LIB = os.path.join(HERE, "libmsm_mi355x.so")
+# MSM_BUILD_VARIANT=<tag>: objects in _build_<tag>, library tools/ablib/libmsm_<tag>.so
+# (A/B variants built with MSM_EXTRA_FLAGS; the product build leaves both unset)
+_VAR = os.environ.get("MSM_BUILD_VARIANT")
+OBJ = os.path.join(HERE, "_build" + (f"_{_VAR}" if _VAR else ""))
+LIB = (os.path.join(os.path.dirname(HERE), "tools", "ablib", f"libmsm_{_VAR}.so") if _VAR
+       else os.path.join(HERE, "libmsm_mi355x.so"))
 BIN = os.path.join(HERE, "bin")
 REPO = os.path.dirname(HERE)
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("MSM_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-value",
-         "-Wno-unused-function", f"-I{os.path.join(REPO, 'include')}"]
+         "-Wno-unused-function", f"-I{os.path.join(REPO, 'include')}"] + os.environ.get("MSM_EXTRA_FLAGS", "").split()
 # (source, MSM_GROUP or None): the group-templated engines compile once per
 # group in parallel (the G2 instantiations dominate the build time)
 SOURCES = [("engine.hip", 1), ("engine.hip", 2), ("ches.hip", 1), ("ches.hip", 2), ("bgmw.hip", 1), ("bgmw.hip", 2),
@@ -41,6 +45,7 @@ def _stale(target, inputs):
 
 def build(verbose=False, jobs=5):
     os.makedirs(OBJ, exist_ok=True)
+    os.makedirs(os.path.dirname(LIB), exist_ok=True)
     hdrs = _deps()
     jobs_list = []
     objs = []
@@ -67,6 +72,8 @@ def build(verbose=False, jobs=5):
         list(ex.map(run, jobs_list))
     if jobs_list or _stale(LIB, objs):
         run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", LIB] + objs)
+    if _VAR:
+        return LIB
     # the reference-driver executables (ref main_p1.cpp / main_p2.cpp), host C++ on the C ABI
     drv = os.path.join(HERE, "driver", "ches_driver.cpp")
     hdr = os.path.join(REPO, "include", "msm_ches_driver.hpp")

@@ -20,7 +20,13 @@
 // two hipcub scan kernels, coarse, fine, scatter): every launch that runs
 // beside a batch accumulation costs it ~10-20 us, so the total,
 // the counter clears and the class scan ride in the kernels above instead of
-// launches of their own.
+// launches of their own.  Several independent sets (the MSMs of a batch front
+// group, Ches::run_batch) sort in the same seven launches: blockIdx.y is the
+// set, each set has its own ne input entries (keys + set ne), its own slots
+// of the histogram (set-major, so ONE exclusive scan yields global offsets and
+// the sets' outputs land consecutively in okeys / sorted), its own nb counts /
+// offsets / order entries (offsets are global positions in `sorted`) and its
+// own 512 class counters.
 //
 // fb_bits is chosen per problem so that there are ~256 coarse bins: few enough
 // that a tile's writes to one bin form runs of tens of entries (the L2 merges
@@ -48,8 +54,10 @@ static __global__ void __launch_bounds__(256)
     k_bs_hist(const uint32_t *__restrict__ keys, size_t ne, int fb_bits, int ncb, int ntiles,
               uint32_t *__restrict__ ghist, uint32_t *__restrict__ classes) {
   __shared__ uint32_t h[BS_MAX_CB];
+  keys += (size_t)blockIdx.y * ne;
+  ghist += (size_t)blockIdx.y * ncb * ntiles;
   if (blockIdx.x == 0)
-    for (int c = threadIdx.x; c < 512; c += blockDim.x) classes[c] = 0;
+    for (int c = threadIdx.x; c < 512; c += blockDim.x) classes[(size_t)blockIdx.y * 512 + c] = 0;
   for (int b = threadIdx.x; b < ncb; b += blockDim.x) h[b] = 0;
   __syncthreads();
   const size_t t0 = (size_t)blockIdx.x * BS_TILE;
@@ -108,6 +116,9 @@ static __global__ void __launch_bounds__(256)
   extern __shared__ uint32_t sm[];
   __shared__ uint32_t wsum[4];
   uint32_t *loff = sm, *gb = sm + ncb, *sk = sm + 2 * ncb, *sv = sk + BS_TILE;
+  keys += (size_t)blockIdx.y * ne;
+  vals += (size_t)blockIdx.y * ne;
+  gbase += (size_t)blockIdx.y * ncb * ntiles;
   for (int b = threadIdx.x; b < ncb; b += blockDim.x) {
     loff[b] = 0;
     gb[b] = gbase[(size_t)b * ntiles + blockIdx.x];
@@ -200,7 +211,7 @@ static __global__ void __launch_bounds__(1024)
     k_bs_fine(const uint32_t *__restrict__ okeys, const uint32_t *__restrict__ ovals, int fb_bits, int ncb,
               int ntiles, const uint32_t *__restrict__ gbase, const uint32_t *__restrict__ ghist, uint32_t nb,
               uint32_t *__restrict__ sorted, uint32_t *__restrict__ counts, uint32_t *__restrict__ offsets,
-              uint32_t *__restrict__ class_total) {
+              uint32_t *__restrict__ class_total, int nsets) {
   __shared__ uint32_t off[1 << BS_MAX_FB_BITS];
   __shared__ uint8_t win[1 << BS_MAX_FB_BITS];
   __shared__ uint32_t stage[BS_FINE_CAP];
@@ -209,10 +220,15 @@ static __global__ void __launch_bounds__(1024)
   __shared__ uint32_t cls[256];
   const int FB = 1 << fb_bits;
   const uint32_t fmask = (uint32_t)FB - 1u;
-  const int b = blockIdx.x;
-  const size_t last = (size_t)ncb * ntiles - 1;  // the last (bin, tile) slot ends the valid entries
-  const uint32_t lo = gbase[(size_t)b * ntiles];
-  const uint32_t hi = b + 1 < ncb ? gbase[(size_t)(b + 1) * ntiles] : gbase[last] + ghist[last];
+  const int b = blockIdx.x, set = blockIdx.y;
+  const size_t per = (size_t)ncb * ntiles, s0 = (size_t)set * per;
+  const size_t last = (size_t)nsets * per - 1;  // the last (set, bin, tile) slot ends the valid entries
+  const uint32_t lo = gbase[s0 + (size_t)b * ntiles];
+  const uint32_t hi = b + 1 < ncb ? gbase[s0 + (size_t)(b + 1) * ntiles]
+                                  : (set + 1 < nsets ? gbase[s0 + per] : gbase[last] + ghist[last]);
+  counts += (size_t)set * nb;
+  offsets += (size_t)set * nb;
+  class_total += (size_t)set * 512;
   const uint32_t nbin = hi - lo;
   for (int f = threadIdx.x; f < FB; f += blockDim.x) off[f] = 0;
   if (threadIdx.x < 256) cls[threadIdx.x] = 0;
@@ -319,6 +335,9 @@ static __global__ void __launch_bounds__(256)
   __shared__ uint32_t h[256];
   __shared__ uint32_t base[256];
   __shared__ uint32_t wsum[4];
+  counts += (size_t)blockIdx.y * nb;
+  order += (size_t)blockIdx.y * nb;
+  class_total += (size_t)blockIdx.y * 512;
   const uint32_t t = threadIdx.x, b0 = blockIdx.x * SCHED_PER_BLOCK, lane = t & 63, wave = t >> 6;
   h[t] = 0;
   // exclusive scan of the class totals: one value per thread, wave scans + 4 wave sums

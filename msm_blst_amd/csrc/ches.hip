@@ -623,19 +623,20 @@ void Ches<G>::get_table(void *out, size_t first, size_t count, hipStream_t s) {
 }
 
 template <int G>
-void Ches<G>::digits_sort(hipStream_t s, const uint8_t *d_scalars, size_t stride, int set) {
+void Ches<G>::digits_sort(hipStream_t s, const uint8_t *d_scalars, size_t stride, size_t set_stride, int nsets,
+                          int set) {
   const size_t n = n_, h = (size_t)p_.h, ne = n * h, NB = bucket_count();
   ChesFrontSet &f = fs_[set];
-  f.keys.ensure(ne * 4);
-  f.vals.ensure(ne * 4);
-  f.sorted.ensure(ne * 4);
-  f.counts.ensure(NB * 4);
-  f.offsets.ensure(NB * 4);
-  f.order.ensure(NB * 4);
+  f.keys.ensure(ne * nsets * 4);
+  f.vals.ensure(ne * nsets * 4);
+  f.sorted.ensure(ne * nsets * 4);
+  f.counts.ensure(NB * nsets * 4);
+  f.offsets.ensure(NB * nsets * 4);
+  f.order.ensure(NB * nsets * 4);
 #define MSM_CHES_DIGITS(HT)                                                                                   \
-  hipLaunchKernelGGL(k_ches_digits<HT>, dim3(nblk(n, 256)), dim3(256), 0, s, d_scalars, stride, n, p_.q_exp, p_.h, \
-                     code_.as<uint32_t>(), rank_.as<uint2>(), f.keys.as<uint32_t>(), f.vals.as<uint32_t>(), (uint32_t)B_.size(),  \
-                     (uint32_t)small_, (uint32_t)copies_)
+  hipLaunchKernelGGL(k_ches_digits<HT>, dim3(nblk(n, 256), nsets), dim3(256), 0, s, d_scalars, stride, n, p_.q_exp, \
+                     p_.h, code_.as<uint32_t>(), rank_.as<uint2>(), f.keys.as<uint32_t>(), f.vals.as<uint32_t>(),     \
+                     (uint32_t)B_.size(), (uint32_t)small_, (uint32_t)copies_, set_stride)
   switch (p_.h) {  // the h of the reference configurations (ches_config_files)
     case 12: MSM_CHES_DIGITS(12); break;
     case 13: MSM_CHES_DIGITS(13); break;
@@ -649,17 +650,18 @@ void Ches<G>::digits_sort(hipStream_t s, const uint8_t *d_scalars, size_t stride
   MSM_HIP_CHECK(hipGetLastError());
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[1], s));
   f.sort.run(s, f.keys.as<uint32_t>(), f.vals.as<uint32_t>(), ne, (uint32_t)NB, f.sorted.as<uint32_t>(),
-             f.counts.as<uint32_t>(), f.offsets.as<uint32_t>(), f.order.as<uint32_t>());
+             f.counts.as<uint32_t>(), f.offsets.as<uint32_t>(), f.order.as<uint32_t>(), nsets);
 }
 
 template <int G>
-void Ches<G>::accumulate(hipStream_t s, int set, int bset) {
+void Ches<G>::accumulate(hipStream_t s, int set, int r, int bset) {
   typedef typename FieldOf<G>::F F;
   const size_t NB = bucket_count();
   ChesFrontSet &f = fs_[set];
   buckets_[bset].ensure(NB * sizeof(Xyzz<F>));
-  launch_accumulate<G>(s, f.order.as<uint32_t>(), f.counts.as<uint32_t>(), f.offsets.as<uint32_t>(),
-                       f.sorted.as<uint32_t>(), table_.as<AffP<F>>(), buckets_[bset].as<Xyzz<F>>(), NB);
+  launch_accumulate<G>(s, f.order.as<uint32_t>() + r * NB, f.counts.as<uint32_t>() + r * NB,
+                       f.offsets.as<uint32_t>() + r * NB, f.sorted.as<uint32_t>(), table_.as<AffP<F>>(),
+                       buckets_[bset].as<Xyzz<F>>(), NB);
   MSM_HIP_CHECK(hipGetLastError());
 }
 
@@ -672,9 +674,9 @@ void Ches<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, hfp::J
     return;
   }
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[0], s));
-  digits_sort(s, d_scalars, stride, 0);
+  digits_sort(s, d_scalars, stride, 0, 1, 0);
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[2], s));
-  accumulate(s, 0, 0);
+  accumulate(s, 0, 0, 0);
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[3], s));
   red_.launch(s, buckets_[0].p);
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[4], s));
@@ -737,6 +739,11 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
     MSM_HIP_CHECK(hipHostMalloc(&host_out_, bytes, hipHostMallocDefault));
     host_out_bytes_ = bytes;
   }
+  // front groups: [0, 1), then up to kFrontGroup MSMs each.  The first group is a
+  // single MSM so the first accumulation starts after one front, not eight.
+  std::vector<size_t> fgb{0};
+  while (fgb.back() < count) fgb.push_back(std::min(count, fgb.back() == 0 ? (size_t)1 : fgb.back() + kFrontGroup));
+  const size_t nfg = fgb.size() - 1;
   // every buffer the loop touches exists before the first launch (an allocation
   // inside the issue loop could synchronise the device)
   const size_t NB = bucket_count(), n = n_;
@@ -744,8 +751,19 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
   // sized for kGroup whatever this batch's R: a later, larger batch must not
   // reallocate (a hipFree inside the pipelined region would synchronise it)
   for (int t = 0; t < kBSets && (size_t)t < ngroups; ++t) red_.ensure_group(t, kGroup);
-  if (scalars_on_host)
-    for (int f = 0; f < kSlots; ++f) scal_[f].ensure(n * stride + 16);
+  // front sets sized for a whole front group (the sort's scan scratch too): run
+  // one sort of kFrontGroup sets per set before the loop if they are not yet
+  // sized (kFrontGroup dummy sets of all-zero scalars, outside the batch timing)
+  const size_t sslot = n * stride;  // one device scalar slot
+  if (scalars_on_host || fs_[0].sorted.bytes < n * (size_t)p_.h * kFrontGroup * 4) {
+    scal_.ensure(2 * kFrontGroup * sslot + 16);
+  }
+  for (int f = 0; f < kFronts && (size_t)f < nfg; ++f)
+    if (fs_[f].sorted.bytes < n * (size_t)p_.h * kFrontGroup * 4) {
+      MSM_HIP_CHECK(hipMemsetAsync(scal_.p, 0, kFrontGroup * sslot, s));
+      digits_sort(s, scal_.as<uint8_t>(), stride, sslot, kFrontGroup, f);
+      MSM_HIP_CHECK(hipStreamSynchronize(s));
+    }
   const bool prof = profile_;
   profile_ = false;
   if (prof)
@@ -754,81 +772,85 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
       MSM_HIP_CHECK(hipEventCreate(&e));
       acc_ev_.push_back(e);
     }
-  // Streams, kFronts front sets (k % kFronts), kBSets bucket sets (k % kBSets)
-  // and, for host scalars, kSlots device scalar slots (k % kSlots):
-  //   fstream_:  digits + sort of MSM k into front set k % kFronts (after MSM
-  //              k - kFronts's accumulation released it).  The accumulation fills
-  //              every CU slot until its last workgroups are dispatched, so a front
-  //              only gets the chip in an accumulation's tail: with three sets, MSM
-  //              k+1's front runs in MSM k-1's tail and is ready before MSM k's
-  //              accumulation ends;
+  // Streams, front groups g (front set g % kFronts), bucket sets k % kBSets and,
+  // for host scalars, two groups of device scalar slots (g % 2):
+  //   fstream_:  digits + sort of front group g: ONE pass per stage over its R_g
+  //              scalar sets (bucket_sort.hpp), after group g - 2's accumulations
+  //              released the front set.  Issued when group g - 1's accumulations
+  //              are enqueued, so it runs beside them; at the greatest priority,
+  //              its short memory-bound kernels take the CU slots the
+  //              accumulation's retiring workgroups free;
   //   s:         accumulation k into bucket set k % kBSets (after MSM k-2's
   //              reduction head released it) -- back to back, the VALU-bound
   //              critical path;
-  //   tails_[t]: the reductions of group g = k / R, t = g % 2: level 0 of each
-  //              MSM into its slot of reducer set t right after its accumulation,
-  //              then, after the group's last MSM, ONE launch per tail level for
-  //              the whole group and one read-back.  Every launch that runs
-  //              beside an accumulation costs it ~10-20 us (profiles/
-  //              r02_batch_sched2.txt: skipping the per-MSM tail levels sped the
-  //              batch from 2.52 to 2.25 ms per MSM), so the ~35 latency-bound
-  //              levels are paid once per group, not once per MSM (groups of 8:
-  //              2.47 -> 2.35 ms per MSM; 4 and 20 measure the same).  Two streams:
-  //              group g+1's level 0s never queue behind group g's tail;
-  //   cstream_:  host scalars: the H2D copy of set k + kSlots into the slot front
-  //              k has consumed, on its own stream (copies on the front stream:
-  //              -5 %, on the reduction streams: -15 %; own stream: -2 % vs
-  //              resident scalars).
+  //   tails_[t]: the reductions of reduction group q = k / R, t = q % 2: level 0
+  //              of each MSM into its slot of reducer set t right after its
+  //              accumulation, then, after the group's last MSM, ONE launch per
+  //              tail level for the whole group and one read-back.  Every launch
+  //              that runs beside an accumulation costs it ~10-20 us
+  //              (profiles/r02_batch_sched2.txt), so the ~35 latency-bound levels
+  //              are paid once per group, not once per MSM.  Two streams: group
+  //              q+1's level 0s never queue behind group q's tail;
+  //   cstream_:  host scalars: the H2D copies of front group g's sets into slot
+  //              group g % 2, after front g - 2 consumed it, on their own stream.
   // No host waits inside the loop: every MSM has its own pinned read-back slot.
-  // Reducer set t is reused by group g + 2 only after group g's tail: both are
+  // Reducer set t is reused by group q + 2 only after group q's tail: both are
   // in order on tails_[t].
-  while (bev_.size() < 4 * count + 1) {
+  while (bev_.size() < 3 * count + 2 * nfg + 1) {
     hipEvent_t e;
     MSM_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     bev_.push_back(e);
   }
-  hipEvent_t *evf = bev_.data() + 1, *eva = evf + count, *evh = eva + count, *evc = evh + count;
+  hipEvent_t *eva = bev_.data() + 1, *evh = eva + count, *evf = evh + count, *evc = evf + nfg;
   MSM_HIP_CHECK(hipEventRecord(bev_[0], s));  // the batch starts after prior work on s
   MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, bev_[0], 0));
+  MSM_HIP_CHECK(hipStreamWaitEvent(cstream_, bev_[0], 0));
   for (int t = 0; t < kBSets; ++t) MSM_HIP_CHECK(hipStreamWaitEvent(tails_[t], bev_[0], 0));
-  auto copy_set = [&](size_t k) {
-    if (!scalars_on_host || k >= count) return;
-    MSM_HIP_CHECK(hipMemcpyAsync(scal_[k % kSlots].p, scalars + k * set_stride, n * stride, hipMemcpyHostToDevice,
-                                 cstream_));
-    MSM_HIP_CHECK(hipEventRecord(evc[k], cstream_));
+  auto slots = [&](size_t g) { return scal_.as<uint8_t>() + (g % 2) * kFrontGroup * sslot; };
+  auto copy_group = [&](size_t g) {
+    if (!scalars_on_host || g >= nfg) return;
+    if (g >= 2) MSM_HIP_CHECK(hipStreamWaitEvent(cstream_, evf[g - 2], 0));  // slots consumed by front g - 2
+    for (size_t k = fgb[g]; k < fgb[g + 1]; ++k)
+      MSM_HIP_CHECK(hipMemcpyAsync(slots(g) + (k - fgb[g]) * sslot, scalars + k * set_stride, sslot,
+                                   hipMemcpyHostToDevice, cstream_));
+    MSM_HIP_CHECK(hipEventRecord(evc[g], cstream_));
   };
-  for (size_t k = 0; k < (size_t)kSlots; ++k) copy_set(k);
-  for (size_t k = 0; k < count; ++k) {
-    const int bset = (int)(k % kBSets), fset = (int)(k % kFronts);
-    const int slot = (int)(k % R), gset = (int)((k / R) % 2);
-    hipStream_t ts = tails_[gset];
-    const uint8_t *src = scalars + k * set_stride;
-    if (scalars_on_host) {
-      src = scal_[k % kSlots].as<uint8_t>();
-      MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, evc[k], 0));
-    }
-    if (k >= (size_t)kFronts) MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, eva[k - kFronts], 0));  // front set free
-    digits_sort(fstream_, src, stride, fset);
-    MSM_HIP_CHECK(hipEventRecord(evf[k], fstream_));
-    if (scalars_on_host && k + kSlots < count) {  // set k + kSlots into the slot front k has consumed
-      MSM_HIP_CHECK(hipStreamWaitEvent(cstream_, evf[k], 0));
-      copy_set(k + kSlots);
-    }
-    MSM_HIP_CHECK(hipStreamWaitEvent(s, evf[k], 0));
-    if (k >= (size_t)kBSets) MSM_HIP_CHECK(hipStreamWaitEvent(s, evh[k - kBSets], 0));  // bucket set free again
-    if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k], s));
-    accumulate(s, fset, bset);
-    if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k + 1], s));
-    MSM_HIP_CHECK(hipEventRecord(eva[k], s));
-    MSM_HIP_CHECK(hipStreamWaitEvent(ts, eva[k], 0));
-    red_.launch_head_slot(ts, buckets_[bset].p, gset, slot);
-    MSM_HIP_CHECK(hipEventRecord(evh[k], ts));
-    if ((size_t)slot + 1 == R || k + 1 == count) {  // the group's last MSM
-      red_.launch_tail_group(ts, gset, slot + 1);
-      red_.copy_out_group(ts, gset, slot + 1, (uint8_t *)host_out_ + (k - slot) * ob);
+  auto front_group = [&](size_t g) {
+    if (g >= nfg) return;
+    if (scalars_on_host) MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, evc[g], 0));
+    if (g >= (size_t)kFronts) MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, eva[fgb[g - kFronts + 1] - 1], 0));
+    const uint8_t *src = scalars_on_host ? slots(g) : scalars + fgb[g] * set_stride;
+    digits_sort(fstream_, src, stride, scalars_on_host ? sslot : set_stride, (int)(fgb[g + 1] - fgb[g]),
+                (int)(g % kFronts));
+    MSM_HIP_CHECK(hipEventRecord(evf[g], fstream_));
+  };
+  copy_group(0);
+  copy_group(1);
+  front_group(0);
+  for (size_t g = 0; g < nfg; ++g) {
+    front_group(g + 1);  // beside this group's accumulations
+    copy_group(g + 2);
+    MSM_HIP_CHECK(hipStreamWaitEvent(s, evf[g], 0));
+    for (size_t k = fgb[g]; k < fgb[g + 1]; ++k) {
+      const int bset = (int)(k % kBSets), slot = (int)(k % R), gset = (int)((k / R) % 2);
+      hipStream_t ts = tails_[gset];
+      if (k >= (size_t)kBSets) MSM_HIP_CHECK(hipStreamWaitEvent(s, evh[k - kBSets], 0));  // bucket set free again
+      if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k], s));
+      accumulate(s, (int)(g % kFronts), (int)(k - fgb[g]), bset);
+      if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k + 1], s));
+      MSM_HIP_CHECK(hipEventRecord(eva[k], s));
+      MSM_HIP_CHECK(hipStreamWaitEvent(ts, eva[k], 0));
+      red_.launch_head_slot(ts, buckets_[bset].p, gset, slot);
+      MSM_HIP_CHECK(hipEventRecord(evh[k], ts));
+      if ((size_t)slot + 1 == R || k + 1 == count) {  // the reduction group's last MSM
+        red_.launch_tail_group(ts, gset, slot + 1);
+        red_.copy_out_group(ts, gset, slot + 1, (uint8_t *)host_out_ + (k - slot) * ob);
+      }
     }
   }
   // the caller's stream observes completion of every reduction (and front)
+  MSM_HIP_CHECK(hipEventRecord(ev_tail_[0], fstream_));
+  MSM_HIP_CHECK(hipStreamWaitEvent(s, ev_tail_[0], 0));
   for (int t = 0; t < kBSets; ++t) {
     MSM_HIP_CHECK(hipEventRecord(ev_tail_[t], tails_[t]));
     MSM_HIP_CHECK(hipStreamWaitEvent(s, ev_tail_[t], 0));

@@ -206,10 +206,15 @@ template <int HT>
 static __global__ void __launch_bounds__(256)
     k_ches_digits(const uint8_t *__restrict__ scalars, size_t stride, size_t n, int q_exp, int h_rt,
                   const uint32_t *__restrict__ code, const uint2 *__restrict__ rank, uint32_t *__restrict__ keys, uint32_t *__restrict__ vals,
-                  uint32_t nb0, uint32_t small, uint32_t copies) {
+                  uint32_t nb0, uint32_t small, uint32_t copies, size_t set_stride) {
   const int h = HT ? HT : h_rt;
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  // blockIdx.y: scalar set of a batch front group (set_stride bytes apart), its
+  // n h entries at keys / vals + set n h (BucketSort's per-set inputs)
+  scalars += (size_t)blockIdx.y * set_stride;
+  keys += (size_t)blockIdx.y * n * h;
+  vals += (size_t)blockIdx.y * n * h;
   const uint8_t *sp = scalars + i * stride;
   uint32_t s[10];
   if ((stride & 3) == 0) {

@@ -98,13 +98,9 @@ __device__ __forceinline__ void coop_xyzz_add(const Xyzz<F> &a, const Xyzz<F> &b
   } else if (w == 1) {
     const F PPP = coop_get(L, 2, lane), Q = coop_get(L, 3, lane);
     F X3 = coop_get(L, 5, lane), t;  // RR
-    f_sub4(X3, X3, PPP);  // < 6p
-    f_norm(X3);
-    f_sub4(X3, X3, Q);  // < 10p
-    f_norm(X3);
-    f_sub4(X3, X3, Q);  // < 14p
-    f_nred(X3);         // X3 = R^2 - PPP - 2Q   S
-    f_sub4(t, Q, X3);   // < 6p
+    f_sub_2x(X3, X3, PPP, Q);  // R^2 + 8p - PPP - 2Q   < 10p
+    f_norm(X3);         // X3 = R^2 - PPP - 2Q   X (normalized, < 10p)
+    f_sub16(t, Q, X3);  // < 18p
     f_mul_sub(o1, t, R, s1, PPP);  // Y3 = R (Q - X3) - S1 PPP   S
     o0 = X3;
   } else {

@@ -9,7 +9,9 @@
 //   xyzz_dbl   <- the doubling branch of the above, used by the reductions
 // An xyzz point (X, Y, ZZZ, ZZ) stands for (X/ZZ, Y/ZZZ); infinity is ZZ == 0
 // (set exactly, never produced by a product).  Every coordinate leaving these
-// functions is in range class S (normalized, < 2p per component; fp.hpp).
+// functions is in range class S (normalized, < 2p per component; fp.hpp)
+// except x, which is left in class X (normalized, < 10p): it only enters
+// products and the subtrahend of f_sub16, so its reduction is skipped.
 // Branches for the rare cases (P == +-bucket, infinity) are data-dependent
 // and divergent; random inputs never take them, the parity tests force them.
 #pragma once
@@ -69,11 +71,11 @@ MSM_FN void xyzz_dbl(Xyzz<F> &r, const Xyzz<F> &a) {
   f_sqr(M, a.x);           // S
   f_mul3(M, M);            // < 6p lazy
   f_sqr(X3, M);            // S
-  f_sub4(X3, X3, S);       // < 6p
-  f_norm(X3);
-  f_sub4(X3, X3, S);       // < 10p
-  f_nred(X3);              // S
-  f_sub4(t, S, X3);        // < 6p
+  F z;
+  f_zero(z);
+  f_sub_2x(X3, X3, z, S);  // M^2 + 8p - 2S   < 10p
+  f_norm(X3);              // X
+  f_sub16(t, S, X3);       // < 18p
   f_mul_sub(Y3, t, M, W, a.y);  // M (S - X3) - W Y   S (one reduction)
   f_mul(r.zz, V, a.zz);
   f_mul(r.zzz, W, a.zzz);
@@ -97,7 +99,7 @@ MSM_FN void xyzz_madd(Xyzz<F> &acc, const Aff<F> &p, bool neg) {
   }
   f_mul_bs(P, p.x, acc.zz);   // U2 = X2 ZZ1          S
   f_mul_bs(R, y2, acc.zzz);   // S2 = Y2 ZZZ1         S
-  f_sub4(P, P, acc.x);     // P = U2 - X1          < 6p lazy
+  f_sub16(P, P, acc.x);    // P = U2 - X1          < 18p lazy
   f_sub4(R, R, acc.y);     // R = S2 - Y1          < 6p lazy
   f_sqr(PP, P);            // PP                   S
   if (__builtin_expect(f_is_zero_S(PP), 0)) {
@@ -122,13 +124,9 @@ MSM_FN void xyzz_madd(Xyzz<F> &acc, const Aff<F> &p, bool neg) {
   f_mul_bs(acc.zzz, acc.zzz, PPP); // ZZZ3 = ZZZ1 PPP      S
   F X3;
   f_sqr(X3, R);            // R^2                  S
-  f_sub4(X3, X3, PPP);     // < 6p
-  f_norm(X3);
-  f_sub4(X3, X3, acc.x);   // < 10p
-  f_norm(X3);
-  f_sub4(X3, X3, acc.x);   // < 14p
-  f_nred(X3);              // X3 = R^2 - PPP - 2Q  S
-  f_sub4(t, acc.x, X3);    // Q - X3  < 6p
+  f_sub_2x(X3, X3, PPP, acc.x);  // R^2 + 8p - PPP - 2Q   < 10p
+  f_norm(X3);              // X3 = R^2 - PPP - 2Q  X
+  f_sub16(t, acc.x, X3);   // Q - X3  < 18p
   f_mul_sub(acc.y, t, R, acc.y, PPP);  // Y3 = R (Q - X3) - Y1 PPP   S (one reduction)
   acc.x = X3;
 }
@@ -172,13 +170,9 @@ MSM_FN void xyzz_add(Xyzz<F> &acc, const Xyzz<F> &b) {
   f_mul_bs(acc.zzz, acc.zzz, PPP); // ZZZ3 = ZZZ1 ZZZ2 PPP
   F X3;
   f_sqr(X3, R);
-  f_sub4(X3, X3, PPP);
-  f_norm(X3);
-  f_sub4(X3, X3, acc.x);
-  f_norm(X3);
-  f_sub4(X3, X3, acc.x);
-  f_nred(X3);                   // X3 = R^2 - PPP - 2Q  S
-  f_sub4(t, acc.x, X3);
+  f_sub_2x(X3, X3, PPP, acc.x);
+  f_norm(X3);                   // X3 = R^2 - PPP - 2Q  X
+  f_sub16(t, acc.x, X3);
   f_mul_sub(acc.y, t, R, acc.y, PPP);  // Y3 = R (Q - X3) - S1 PPP   S (one reduction)
   acc.x = X3;
 }

@@ -20,36 +20,38 @@ namespace msm {
 
 #if MSM_GROUP == 1  // group-independent: compiled once
 void BucketSort::run(hipStream_t s, const uint32_t *keys, const uint32_t *vals, size_t ne, uint32_t nb,
-                     uint32_t *sorted, uint32_t *counts, uint32_t *offsets, uint32_t *order) {
+                     uint32_t *sorted, uint32_t *counts, uint32_t *offsets, uint32_t *order, int nsets) {
   // ~256 coarse bins (see bucket_sort.hpp), fine buckets per bin in [2^8, 2^12]
   int fb_bits = 8;
   while (fb_bits < BS_MAX_FB_BITS && ((size_t)nb >> fb_bits) > 384) ++fb_bits;
   const int ncb = (int)(((size_t)nb + (1u << fb_bits) - 1) >> fb_bits);
   if (ncb > BS_MAX_CB || ncb > 4096) throw std::runtime_error("BucketSort: too many buckets");
-  if (ne >= (1ull << 32)) throw std::runtime_error("BucketSort: too many entries");
+  if (nsets < 1 || nsets > 65535) throw std::runtime_error("BucketSort: bad set count");
+  if (ne * nsets >= (1ull << 32)) throw std::runtime_error("BucketSort: too many entries");
   const int ntiles = (int)std::max<size_t>(1, (ne + BS_TILE - 1) / BS_TILE);
-  const size_t nslots = (size_t)ncb * ntiles;
+  const size_t nslots = (size_t)nsets * ncb * ntiles;
+  if (nslots >= (1ull << 31)) throw std::runtime_error("BucketSort: too many histogram slots");
   ghist.ensure(nslots * 4);
   gbase.ensure(nslots * 4);
-  okeys.ensure(std::max<size_t>(ne, 1) * 4);
-  ovals.ensure(std::max<size_t>(ne, 1) * 4);
+  okeys.ensure(std::max<size_t>(ne * nsets, 1) * 4);
+  ovals.ensure(std::max<size_t>(ne * nsets, 1) * 4);
   size_t scan_tmp = 0;
   hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, ghist.as<uint32_t>(), gbase.as<uint32_t>(), (int)nslots, s);
   tmp.ensure(scan_tmp);
-  classes.ensure(512 * 4);  // 256 class totals + 256 class cursors, cleared by k_bs_hist's block 0
-  hipLaunchKernelGGL(k_bs_hist, dim3(ntiles), dim3(256), 0, s, keys, ne, fb_bits, ncb, ntiles, ghist.as<uint32_t>(),
-                     classes.as<uint32_t>());
+  classes.ensure((size_t)512 * 4 * nsets);  // per set: 256 class totals + 256 cursors, cleared by k_bs_hist
+  hipLaunchKernelGGL(k_bs_hist, dim3(ntiles, nsets), dim3(256), 0, s, keys, ne, fb_bits, ncb, ntiles,
+                     ghist.as<uint32_t>(), classes.as<uint32_t>());
   MSM_HIP_CHECK(hipGetLastError());
   size_t tb = scan_tmp;
   MSM_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, ghist.as<uint32_t>(), gbase.as<uint32_t>(), (int)nslots, s));
-  hipLaunchKernelGGL(k_bs_coarse, dim3(ntiles), dim3(256), (size_t)(2 * ncb + 2 * BS_TILE) * 4, s, keys, vals, ne,
-                     fb_bits, ncb, ntiles, gbase.as<uint32_t>(), okeys.as<uint32_t>(), ovals.as<uint32_t>());
+  hipLaunchKernelGGL(k_bs_coarse, dim3(ntiles, nsets), dim3(256), (size_t)(2 * ncb + 2 * BS_TILE) * 4, s, keys, vals,
+                     ne, fb_bits, ncb, ntiles, gbase.as<uint32_t>(), okeys.as<uint32_t>(), ovals.as<uint32_t>());
   MSM_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(k_bs_fine, dim3(ncb), dim3(1024), 0, s, okeys.as<uint32_t>(), ovals.as<uint32_t>(), fb_bits, ncb,
-                     ntiles, gbase.as<uint32_t>(), ghist.as<uint32_t>(), nb, sorted, counts, offsets,
-                     classes.as<uint32_t>());
+  hipLaunchKernelGGL(k_bs_fine, dim3(ncb, nsets), dim3(1024), 0, s, okeys.as<uint32_t>(), ovals.as<uint32_t>(),
+                     fb_bits, ncb, ntiles, gbase.as<uint32_t>(), ghist.as<uint32_t>(), nb, sorted, counts, offsets,
+                     classes.as<uint32_t>(), nsets);
   MSM_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(k_sched_scatter, dim3(nblk(nb, SCHED_PER_BLOCK)), dim3(256), 0, s, counts, nb,
+  hipLaunchKernelGGL(k_sched_scatter, dim3(nblk(nb, SCHED_PER_BLOCK), nsets), dim3(256), 0, s, counts, nb,
                      classes.as<uint32_t>(), order);
   MSM_HIP_CHECK(hipGetLastError());
 }

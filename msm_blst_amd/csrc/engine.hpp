@@ -68,9 +68,13 @@ struct HostField<2> {
 // accumulation schedule (bucket ids by descending count).
 struct BucketSort {
   DevBuf ghist, gbase, okeys, ovals, classes, tmp;
-  // keys[ne] (bucket < nb or 0xffffffff), vals[ne]; outputs sized ne / nb
+  // keys[ne] (bucket < nb or 0xffffffff), vals[ne]; outputs sized ne / nb.
+  // nsets > 1: nsets independent sorts in the same launches -- inputs at
+  // keys/vals + r ne, outputs counts/offsets/order + r nb (offsets index the one
+  // shared `sorted` array of up to nsets ne entries), bucket_sort.hpp
   void run(hipStream_t s, const uint32_t *keys, const uint32_t *vals, size_t ne, uint32_t nb, uint32_t *sorted,
-           uint32_t *counts, uint32_t *offsets, uint32_t *order);
+           uint32_t *counts, uint32_t *offsets, uint32_t *order, int nsets = 1);
+  size_t device_bytes() const { return ghist.bytes + gbase.bytes + okeys.bytes + ovals.bytes + classes.bytes + tmp.bytes; }
 };
 
 // Dense windowed bucket reduction: for each of W windows of S buckets
@@ -278,11 +282,13 @@ class Ches {
   // scalars: n 32-byte LE strings (stride >= 32) on device
   void run(hipStream_t s, const uint8_t *d_scalars, size_t stride, hfp::Jac<HF> *out);
   // `count` MSMs over the same points; scalar set k at scalars + k * set_stride,
-  // in device memory or (scalars_on_host) host memory -- then each set is copied
-  // into one of kSlots device slots on its own copy stream (cstream_), ahead of
-  // its digit conversion and overlapping earlier MSMs' accumulations (pinned
-  // host memory for a truly asynchronous copy).  Pipelined: MSM k's reduction
-  // runs on a second stream beside MSM k+1's accumulation.
+  // in device memory or (scalars_on_host) host memory -- then each front group's
+  // sets are copied into device slots on their own copy stream (cstream_), ahead
+  // of the group's front and overlapping earlier accumulations (pinned host
+  // memory for a truly asynchronous copy).  Pipelined: front group g + 1 (digits
+  // + sort of up to kFrontGroup sets in one pass) beside group g's
+  // accumulations, MSM k's reduction on a second stream beside MSM k+1's
+  // accumulation.
   void run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, size_t set_stride, size_t count,
                  hfp::Jac<HF> *outs, bool scalars_on_host = false);
   size_t npoints() const { return n_; }
@@ -308,13 +314,19 @@ class Ches {
   // MSM k-1 still reads the other one
   static constexpr int kBSets = 2;
   DevBuf code_, rank_, table_, buckets_[kBSets];
-  // digit/sort outputs, one set per in-flight front so that MSM k+1's digits
-  // and sort (memory/LDS-bound) run beside MSM k's accumulation (VALU-bound)
-  static constexpr int kGroup = 8;   // batch: MSMs per reduction group (WeightedReducer::launch_tail_group)
-  static constexpr int kFronts = 3;  // batch: front k+1 runs in MSM k-1's accumulation tail
+  // digit/sort outputs.  A batch runs the fronts (digits + sort, memory/LDS-
+  // bound) of up to kFrontGroup MSMs in ONE pass per stage (seven launches for
+  // the group instead of seven per MSM: every launch beside an accumulation
+  // costs it ~10-20 us), front group g+1 beside group g's accumulations; two
+  // front sets alternate between the groups.  The synchronous MSM uses set 0
+  // with one scalar set.
+  static constexpr int kGroup = 8;       // batch: MSMs per reduction group (WeightedReducer::launch_tail_group)
+  static constexpr int kFrontGroup = 8;  // batch: MSMs per front group (the first group holds one MSM)
+  static constexpr int kFronts = 2;
   ChesFrontSet fs_[kFronts];
-  static constexpr int kSlots = 4;   // device slots of host scalar sets in a batch
-  DevBuf scal_[kSlots];
+  // host scalar sets of a batch: two groups of kFrontGroup device slots, copied on
+  // their own stream (cstream_) ahead of the group's front
+  DevBuf scal_;
   WeightedReducer<G> red_;
   std::vector<hipEvent_t> ev_;
   hipStream_t tails_[kBSets] = {nullptr, nullptr}, fstream_ = nullptr, cstream_ = nullptr;  // batch streams (+ the caller's)
@@ -323,8 +335,10 @@ class Ches {
   size_t host_out_bytes_ = 0;
   std::vector<hipEvent_t> bev_;     // batch dependency events, one per (MSM, stage)
   std::vector<hipEvent_t> acc_ev_;  // batch profiling: events around each accumulation
-  void digits_sort(hipStream_t s, const uint8_t *d_scalars, size_t stride, int set);
-  void accumulate(hipStream_t s, int set, int bset);
+  // digits + sort of nsets scalar sets (set_stride bytes apart) into front set `set`
+  void digits_sort(hipStream_t s, const uint8_t *d_scalars, size_t stride, size_t set_stride, int nsets, int set);
+  // accumulation of scalar set r of front set `set` into bucket set bset
+  void accumulate(hipStream_t s, int set, int r, int bset);
 };
 
 // BGMW95 fixed-base variant (ref main_p1.cpp:94-122, 294-398;

@@ -68,6 +68,10 @@ MSM_CONST uint32_t SUB16P[NL] = {0x1ffaaab0, 0x1efffffe, 0x1ffffb9e, 0x1ffeb152,
 MSM_CONST uint32_t SUB32P[NL] = {0x1ff55560, 0x1dfffffe, 0x1ffff73e, 0x1ffd62a6, 0x1483d57e,
                                             0x11ed61eb, 0x1ce61a53, 0x170a257d, 0x1ee9709d, 0x1759aec7,
                                             0x14f6c868, 0x1d349636, 0x1d472ffb, 0x0340222};
+// 8p borrow-adjusted so limbs 0..12 are >= 3(2^28-1): the minuend of fp_sub_2x
+MSM_CONST uint32_t SUB8P3[NL] = {0x3ffd5558, 0x3f7ffffc, 0x3ffffdcc, 0x3fff58a6, 0x3120f55c,
+                                            0x307b5878, 0x3b398692, 0x39c2895c, 0x33ba5c24, 0x35d66baf,
+                                            0x3d3db217, 0x334d258a, 0x3f51cbfc, 0x00d0085};
 // 2^392 mod p (one), 2^400 mod p (blst -> internal), 2^384 mod p (internal -> blst)
 MSM_CONST uint32_t ONE28[NL] = {0x347fcb8, 0xd800000, 0x002b119, 0x0cde6d2, 0xc7212e0, 0x83a2090, 0x037669f,
                                            0xda0f73e, 0x9b09b42, 0x1297bb0, 0x515d98f, 0x012ca7c, 0x659fcfa, 0x000577a};
@@ -255,6 +259,18 @@ MSM_FN void fp_sub(Fp &r, const Fp &a, const Fp &b) {
     r.v[i] = a.v[i] + C[i] - b.v[i];
   }
 }
+// r = a + 8p - b - 2c for b, c normalized (limbs < 2^28) with b + 2c <= 8p:
+// three VALU ops per limb (v_lshl_add_u32, v_sub, v_add) instead of three
+// fp_sub<4> + two fp_norm -- the X3 = R^2 - PPP - 2Q line of the xyzz formulas.
+MSM_FN void fp_sub_2x(Fp &r, const Fp &a, const Fp &b, const Fp &c) {
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const uint32_t t = b.v[i] + (c.v[i] << 1);
+    MSM_CHECK((uint64_t)b.v[i] + 2ull * c.v[i] <= SUB8P3[i]);           // limb >= 0
+    MSM_CHECK((uint64_t)a.v[i] + SUB8P3[i] - t <= 0xffffffffull);       // no wrap
+    r.v[i] = a.v[i] + (SUB8P3[i] - t);
+  }
+}
 // r = K*p - a (negation), a normalized
 template <int K>
 MSM_FN void fp_neg(Fp &r, const Fp &a) {
@@ -345,6 +361,9 @@ MSM_FN void fp_nred(Fp &a) {
 // Range classes used by ec.hpp (all values non-negative):
 //   S : normalized limbs (< 2^28), value < 2p.  Every f_mul/f_sqr output, every
 //       f_nred output, every stored coordinate.
+//   X : normalized limbs, value < 10p: the x coordinate of a stored xyzz point
+//       (X3 = R^2 - PPP - 2Q is normalized but not reduced; x only ever enters
+//       products and the subtrahend of f_sub16).
 //   lazy : limbs < 2^30, value < 40p.  Legal f_mul/f_sqr input.
 //   f_add(S,S) < 4p lazy; f_sub4(x,S) = x + 4p - S (x S -> < 6p lazy);
 //   f_sub subtrahend MUST be S.
@@ -352,6 +371,10 @@ MSM_FN void f_mul(Fp &r, const Fp &a, const Fp &b) { fp_mul(r, a, b); }
 MSM_FN void f_sqr(Fp &r, const Fp &a) { fp_sqr(r, a); }
 MSM_FN void f_add(Fp &r, const Fp &a, const Fp &b) { fp_add(r, a, b); }
 MSM_FN void f_sub4(Fp &r, const Fp &a, const Fp &b) { fp_sub<4>(r, a, b); }
+// a + 8p - b - 2c, b and c in S (b + 2c < 6p) -> lazy (< a + 8p, limbs < 2^31)
+MSM_FN void f_sub_2x(Fp &r, const Fp &a, const Fp &b, const Fp &c) { fp_sub_2x(r, a, b, c); }
+// a + 16p - b for b normalized < 16p (class X: the lazily reduced x coordinate)
+MSM_FN void f_sub16(Fp &r, const Fp &a, const Fp &b) { fp_sub<16>(r, a, b); }
 MSM_FN void f_nred(Fp &a) { fp_nred(a); }
 MSM_FN void f_norm(Fp &a) { fp_norm(a); }
 MSM_FN void f_neg4(Fp &r, const Fp &a) { fp_neg<4>(r, a); }
@@ -413,14 +436,15 @@ MSM_FN void f_mul_bs(Fp &r, const Fp &a, const Fp &b) { fp_mul(r, a, b); }
 // (a0 + a1 i)^2 = (a0+a1)(a0-a1) + 2 a0 a1 i   (ref no_asm.h:638-688)
 // Both components are normalized first: with lazy inputs (limbs < 3 2^28) the
 // product s d would reach 14 (6 2^28)(5 2^28) > 2^64 in a column (DESIGN 4a,
-// tests/fp_bounds.py); normalized, s limbs < 2^29 and d limbs < 3 2^28.
-// Callers pass values < 6p, so 16p - a1 > 0.
+// tests/fp_bounds.py); normalized, s limbs < 2^29 and d limbs < 2^30.
+// Callers pass values < 18p (P = U2 - X1, X1 in class X), so 32p - a1 > 0 and
+// s d < 36p 50p < 2^392 p.
 MSM_FN void f_sqr(Fp2 &r, const Fp2 &a) {
   Fp s, d, m, a0 = a.c0, a1 = a.c1;
   fp_norm(a0);
   fp_norm(a1);
   fp_add(s, a0, a1);
-  fp_sub<16>(d, a0, a1);
+  fp_sub<32>(d, a0, a1);
   fp_mul(m, a0, a1);
   fp_mul(r.c0, s, d);
   fp_add(r.c1, m, m);
@@ -434,6 +458,14 @@ MSM_FN void f_add(Fp2 &r, const Fp2 &a, const Fp2 &b) {
 MSM_FN void f_sub4(Fp2 &r, const Fp2 &a, const Fp2 &b) {
   fp_sub<4>(r.c0, a.c0, b.c0);
   fp_sub<4>(r.c1, a.c1, b.c1);
+}
+MSM_FN void f_sub16(Fp2 &r, const Fp2 &a, const Fp2 &b) {
+  fp_sub<16>(r.c0, a.c0, b.c0);
+  fp_sub<16>(r.c1, a.c1, b.c1);
+}
+MSM_FN void f_sub_2x(Fp2 &r, const Fp2 &a, const Fp2 &b, const Fp2 &c) {
+  fp_sub_2x(r.c0, a.c0, b.c0, c.c0);
+  fp_sub_2x(r.c1, a.c1, b.c1, c.c1);
 }
 MSM_FN void f_nred(Fp2 &a) { fp_nred(a.c0); fp_nred(a.c1); }
 MSM_FN void f_norm(Fp2 &a) { fp_norm(a.c0); fp_norm(a.c1); }

@@ -62,14 +62,15 @@ MSM_FN void f_mul_bs(Fp2L &r, const Fp2L &a, const Fp2L &b) {
   fp_mul2(t, X, b.c, Z, W);
   r.c = t;
 }
-// (a0 + a1 i)^2: c0 = (a0 + a1)(a0 + 16p - a1), c1 = a0 (2 a1), inputs < 6p
+// (a0 + a1 i)^2: c0 = (a0 + a1)(a0 + 32p - a1), c1 = a0 (2 a1), inputs < 18p
+// (P = U2 - X1 with X1 in class X; tests/fp_bounds.py sqr_fp2l)
 MSM_FN void f_sqr(Fp2L &r, const Fp2L &a) {
   const bool odd = pair_odd();
   Fp own = a.c, par, s, d, X, Y;
   fp_norm(own);
   pair_swap(par, own);
   fp_add(s, own, par);       // even: a0 + a1
-  fp_sub<16>(d, own, par);   // even: a0 + 16p - a1
+  fp_sub<32>(d, own, par);   // even: a0 + 32p - a1
   fp_add(Y, own, own);       // odd: 2 a1 (limbs < 2^29)
   pair_sel(X, odd, par, s);
   pair_sel(Y, odd, Y, d);
@@ -77,6 +78,8 @@ MSM_FN void f_sqr(Fp2L &r, const Fp2L &a) {
 }
 MSM_FN void f_add(Fp2L &r, const Fp2L &a, const Fp2L &b) { fp_add(r.c, a.c, b.c); }
 MSM_FN void f_sub4(Fp2L &r, const Fp2L &a, const Fp2L &b) { fp_sub<4>(r.c, a.c, b.c); }
+MSM_FN void f_sub_2x(Fp2L &r, const Fp2L &a, const Fp2L &b, const Fp2L &c) { fp_sub_2x(r.c, a.c, b.c, c.c); }
+MSM_FN void f_sub16(Fp2L &r, const Fp2L &a, const Fp2L &b) { fp_sub<16>(r.c, a.c, b.c); }
 MSM_FN void f_nred(Fp2L &a) { fp_nred(a.c); }
 MSM_FN void f_norm(Fp2L &a) { fp_norm(a.c); }
 MSM_FN void f_neg4(Fp2L &r, const Fp2L &a) { fp_neg<4>(r.c, a.c); }

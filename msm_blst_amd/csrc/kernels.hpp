@@ -252,11 +252,15 @@ static __global__ void k_iota(uint32_t *a, size_t n) {
   if (i < n) a[i] = (uint32_t)i;
 }
 
+// waves per SIMD the G1 accumulation is compiled for (VGPR budget 512 / waves)
+#ifndef MSM_ACC_WAVES
+#define MSM_ACC_WAVES 3
+#endif
 // One lane per bucket, buckets visited in the schedule `order` (descending
 // entry count, BucketSort) so the 64 lanes of a wave run loops of nearly equal
 // length and the longest buckets start first.
 template <int G, class PT = Aff<typename FieldOf<G>::F>>
-__global__ void __launch_bounds__(256) k_accumulate(const uint32_t *__restrict__ order,
+__global__ void __launch_bounds__(256, MSM_ACC_WAVES) k_accumulate(const uint32_t *__restrict__ order,
                                                     const uint32_t *__restrict__ counts,
                                                     const uint32_t *__restrict__ offsets,
                                                     const uint32_t *__restrict__ sorted,

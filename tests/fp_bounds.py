@@ -40,6 +40,8 @@ def _consts():
 C = _consts()
 P28 = C["P28"]
 SUB = {4: C["SUB4P"], 8: C["SUB8P"], 16: C["SUB16P"], 32: C["SUB32P"]}
+SUB8P3 = C["SUB8P3"]
+assert sum(l << (28 * i) for i, l in enumerate(SUB8P3)) == 8 * P
 RED_MAG = C["RED_MAG"]
 assert sum(l << (28 * i) for i, l in enumerate(P28)) == P
 for k, cs in SUB.items():
@@ -70,6 +72,9 @@ class Iv:
     def is_S(self):
         return all(l < M for l in self.lim[:NL - 1]) and self.vmax < 2 * P
 
+    def is_X(self):
+        return all(l < M for l in self.lim[:NL - 1]) and self.vmax < 10 * P
+
     def __repr__(self):
         return f"Iv(limbs<=2^{max(l.bit_length() for l in self.lim)}, v<{self.vmax / P:.4f}p)"
 
@@ -77,6 +82,12 @@ class Iv:
 def S():
     """class S: normalized limbs, value < 2p (every stored coordinate)"""
     return Iv([M - 1] * (NL - 1) + [(2 * P - 1) >> 364], 2 * P - 1)
+
+
+def Xc():
+    """class X: normalized limbs, value < 10p (the stored x coordinate: X3 is
+    normalized but not reduced)"""
+    return Iv([M - 1] * (NL - 1) + [(10 * P - 1) >> 364], 10 * P - 1)
 
 
 def canonical():
@@ -180,6 +191,19 @@ def sub(a, b, K=4):
     return Iv(lim, a.vmax + K * P)
 
 
+def sub2x(a, b, c):
+    """fp_sub_2x: a + 8p (limbs adjusted to >= 3(2^28-1)) - b - 2c, b and c normalized"""
+    need(all(b.lim[i] + 2 * c.lim[i] <= SUB8P3[i] for i in range(NL)), "fp_sub_2x: negative limb")
+    need(b.vmax + 2 * c.vmax <= 8 * P, "fp_sub_2x: subtrahend above 8p")
+    lim = [a.lim[i] + SUB8P3[i] for i in range(NL)]
+    need(all(l < U32 for l in lim), "fp_sub_2x: limb wraps")
+    return Iv(lim, a.vmax + 8 * P)
+
+
+def zero():
+    return Iv([0] * NL, 0)
+
+
 def neg(a, K=4):
     cs = SUB[K]
     need(all(a.lim[i] <= cs[i] for i in range(NL)), f"fp_neg<{K}>: negative limb")
@@ -227,10 +251,10 @@ def mul_bs_fp2(a, b):      # f_mul_bs(Fp2): b normalized already
     return union(mul2(a, b, a, neg(b, 8)), mul2(a, b, a, b))
 
 
-def sqr_fp2(a):            # f_sqr(Fp2): both normalized, (a0+a1)(a0-a1), 2 a0 a1 (red + norm)
+def sqr_fp2(a):            # f_sqr(Fp2): both normalized, (a0+a1)(a0+32p-a1), 2 a0 a1 (red + norm)
     an = norm(a)
     s = add(an, an)
-    d = sub(an, an, 16)
+    d = sub(an, an, 32)
     m_ = mul(an, an)
     c0 = mul(s, d)
     c1 = norm(red(add(m_, m_)))
@@ -238,8 +262,8 @@ def sqr_fp2(a):            # f_sqr(Fp2): both normalized, (a0+a1)(a0-a1), 2 a0 a
 
 
 def sqr_fp2l(a):           # f_sqr(Fp2L, fp2l.hpp): own component normalized, partner swapped in;
-    an = norm(a)           # even lane (a0 + a1)(a0 + 16p - a1), odd lane a0 (2 a1), one fp_mul each
-    return union(mul(add(an, an), sub(an, an, 16)), mul(an, add(an, an)))
+    an = norm(a)           # even lane (a0 + a1)(a0 + 32p - a1), odd lane a0 (2 a1), one fp_mul each
+    return union(mul(add(an, an), sub(an, an, 32)), mul(an, add(an, an)))
 
 
 def mul_sub_fp2(a, b, c, d):   # f_mul_sub(Fp2): two fp_mul4 with 8p-adjusted negations
@@ -272,30 +296,20 @@ class Field:
 
 # ------------------------------------------------------ formula traces ------
 def _x3(F, R_, PPP, Q):
-    X3 = F.sqr(R_)
-    X3 = sub(X3, PPP)
-    X3 = norm(X3)
-    X3 = sub(X3, Q)
-    X3 = norm(X3)
-    X3 = sub(X3, Q)
-    return nred(X3)
+    return norm(sub2x(F.sqr(R_), PPP, Q))     # f_sub_2x then f_norm: class X
 
 
 def trace_dbl(group, a=None):
     """xyzz_dbl (ec.hpp) of an S point"""
     F = Field(group)
-    x, y, zzz, zz = a or (S(), S(), S(), S())
+    x, y, zzz, zz = a or (Xc(), S(), S(), S())
     U = add(y, y)
     V = F.sqr(U)
     W = F.mul(V, U)
     Sx = F.mul(x, V)
     Mm = mul3(F.sqr(x))
-    X3 = F.sqr(Mm)
-    X3 = sub(X3, Sx)
-    X3 = norm(X3)
-    X3 = sub(X3, Sx)
-    X3 = nred(X3)
-    t = sub(Sx, X3)
+    X3 = norm(sub2x(F.sqr(Mm), zero(), Sx))
+    t = sub(Sx, X3, 16)
     Y3 = F.mul_sub(t, Mm, W, y)
     return X3, Y3, F.mul(W, zzz), F.mul(V, zz)
 
@@ -303,10 +317,10 @@ def trace_dbl(group, a=None):
 def trace_madd(group, negate):
     """xyzz_madd (ec.hpp): S bucket += +-P, P canonical affine; both branches"""
     F = Field(group)
-    x, y, zzz, zz = S(), S(), S(), S()
+    x, y, zzz, zz = Xc(), S(), S(), S()
     px, py = canonical(), canonical()
     y2 = neg(py) if negate else py
-    Pd = sub(F.mul_bs(px, zz), x)
+    Pd = sub(F.mul_bs(px, zz), x, 16)
     Rd = sub(F.mul_bs(y2, zzz), y)
     PP = F.sqr(Pd)
     need(PP.is_S(), "madd: PP must be S for f_is_zero_S")
@@ -315,7 +329,7 @@ def trace_madd(group, negate):
     Q = F.mul_bs(x, PP)
     zzz3 = F.mul_bs(zzz, PPP)
     X3 = _x3(F, Rd, PPP, Q)
-    t = sub(Q, X3)
+    t = sub(Q, X3, 16)
     Y3 = F.mul_sub(t, Rd, y, PPP)
     # doubling branch: b = xyzz_from_aff(P, neg) (y negated then nred, ZZ = ZZZ = one), then dbl
     by = nred(neg(py)) if negate else py
@@ -327,8 +341,8 @@ def trace_madd(group, negate):
 def trace_add(group):
     """xyzz_add (ec.hpp), in place: acc (S) += b (S)"""
     F = Field(group)
-    x, y, zzz, zz = S(), S(), S(), S()
-    bx, by, bzzz, bzz = S(), S(), S(), S()
+    x, y, zzz, zz = Xc(), S(), S(), S()
+    bx, by, bzzz, bzz = Xc(), S(), S(), S()
     U1 = F.mul_bs(x, bzz)
     S1 = F.mul_bs(y, bzzz)
     Pd = sub(F.mul_bs(bx, zz), U1)
@@ -342,7 +356,7 @@ def trace_add(group):
     Q = F.mul_bs(U1, PP)
     zzz3 = F.mul_bs(zzz12, PPP)
     X3 = _x3(F, Rd, PPP, Q)
-    t = sub(Q, X3)
+    t = sub(Q, X3, 16)
     Y3 = F.mul_sub(t, Rd, S1, PPP)
     # doubling branch: acc rewritten as (U1, S1, ZZZ1 ZZZ2, ZZ1 ZZ2), all S, then doubled
     dbl = trace_dbl(group, (U1, S1, zzz12, zz12))
@@ -352,21 +366,16 @@ def trace_add(group):
 def trace_coop_add(group):
     """coop_xyzz_add (coop.hpp): the same add split over 4 waves, f_mul throughout"""
     F = Field(group)
-    ax, ay, azzz, azz = S(), S(), S(), S()
-    bx, by, bzzz, bzz = S(), S(), S(), S()
+    ax, ay, azzz, azz = Xc(), S(), S(), S()
+    bx, by, bzzz, bzz = Xc(), S(), S(), S()
     U1, S1, U2, S2 = F.mul(ax, bzz), F.mul(ay, bzzz), F.mul(bx, azz), F.mul(by, azzz)
     Pd, Rd = sub(U2, U1), sub(S2, S1)
     PP, RR, zz12, zzz12 = F.mul(Pd, Pd), F.mul(Rd, Rd), F.mul(azz, bzz), F.mul(azzz, bzzz)
     need(PP.is_S() and RR.is_S(), "coop: PP, RR must be S")
     PPP, Q, zz3 = F.mul(Pd, PP), F.mul(U1, PP), F.mul(zz12, PP)
     zzz3 = F.mul(zzz12, PPP)
-    X3 = sub(RR, PPP)
-    X3 = norm(X3)
-    X3 = sub(X3, Q)
-    X3 = norm(X3)
-    X3 = sub(X3, Q)
-    X3 = nred(X3)
-    t = sub(Q, X3)
+    X3 = norm(sub2x(RR, PPP, Q))
+    t = sub(Q, X3, 16)
     Y3 = F.mul_sub(t, Rd, S1, PPP)
     return X3, Y3, zzz3, zz3
 
@@ -396,15 +405,18 @@ def prove_all():
     res["G2-pairs xyzz_dbl"] = list(trace_dbl(3))
     for name, outs in res.items():
         for k, o in enumerate(outs):
-            need(o.is_S(), f"{name}: output {'x y zzz zz'.split()[k]} not in class S: {o}")
+            if k == 0:
+                need(o.is_X(), f"{name}: output x not in class X: {o}")
+            else:
+                need(o.is_S(), f"{name}: output {'x y zzz zz'.split()[k]} not in class S: {o}")
     return res
 
 
 def red_report():
     """the fp_red bound for its two kinds of callers"""
-    lazy14 = sub(norm(sub(norm(sub(S(), S())), S())), S())   # shape of the X3 chain input
+    lazy14 = sub2x(S(), S(), S())   # shape of the X3 chain input (f_sub_2x)
     rows = []
-    for name, x in (("X3 chain (< 14p, normalized)", norm(lazy14)),
+    for name, x in (("X3 chain (< 10p, normalized)", norm(lazy14)),
                     ("normalized < 32p", Iv([M - 1] * NL, 32 * P - 1)),
                     ("m + m, limbs < 2^29 (Fp2 sqr)", add(S(), S()))):
         r = red(x)

@@ -47,6 +47,8 @@ void h_fp_op(int op, uint32_t *r, const uint32_t *a, const uint32_t *b, const ui
     case 7: fp_sub<8>(R, ld(a), ld(b)); break;
     case 8: fp_sub<32>(R, ld(a), ld(b)); break;
     case 9: f_mul_sub(R, ld(a), ld(b), ld(c), ld(d)); break;
+    case 10: fp_sub_2x(R, ld(a), ld(b), ld(c)); break;
+    case 11: fp_sub<16>(R, ld(a), ld(b)); break;
     default: return;
   }
   st(r, R);

@@ -6,7 +6,7 @@ proven and then exercised at their bounds on the CPU (no GPU needed).
    point formulas produce, that fp_red (checked exhaustively over its top
    limb) leaves a value in [0, 2p), and that every stored coordinate of every
    formula (G1, G2, main and doubling branches, the 4-wave cooperative add) is
-   in range class S.  DESIGN.md section 4a records the same table.
+   in range class S, except x, which is in class X (normalized, < 10p).  DESIGN.md section 4a records the same table.
 2. The SAME header text (msm_blst_amd/csrc/fp.hpp, ec.hpp) is compiled for the
    host with every range check enabled (tests/host/fp_host_shim.cpp,
    MSM_FP_HOST_TEST) and run on max-limb operands of every range class and on
@@ -50,7 +50,7 @@ def test_interval_model_proves_every_formula():
     res = fb.prove_all()
     assert len(res) == 16 + 7  # G1, G2 (one lane), G2 on lane pairs
     for name, outs in res.items():
-        assert all(o.is_S() for o in outs), name
+        assert outs[0].is_X() and all(o.is_S() for o in outs[1:]), name
 
 
 def test_fp_red_exhaustive_bound():
@@ -122,16 +122,21 @@ def test_fp_primitives_at_class_bounds(shim, seed):
         (6, (lazy, S), (_val(lazy) - _val(S)) % P),
         (5, (lazy14,), _val(lazy14) % P),
         (4, (_maxlimb(fb.Iv([M28] * NL, 32 * P - 1), rnd),), None),
+        (10, (S, S, S), (_val(S) - 3 * _val(S)) % P),                     # X3 line: R^2 - PPP - 2Q
+        (11, (S, _maxlimb(fb.Xc(), rnd)), None),                          # P = U2 - X1, X1 in class X
     ]
     for op, args, want in cases:
         r = _run_fp(shim, op, *args)
         assert shim.h_overflow(1) == 0, (op, args)
-        if op != 6:  # products and reductions land in class S; fp_sub<4> stays lazy
-            assert all(x <= M28 for x in r[:NL - 1]) and _val(r) < 2 * P, op
-        else:
+        if op == 6:
             assert _val(r) < 10 * P   # lazy (< 6p) + 4p - S
+        elif op in (10, 11):
+            assert all(x < (1 << 31) for x in r) and _val(r) < 18 * P, op   # lazy, limbs < 2^31
+        else:  # products and reductions land in class S
+            assert all(x <= M28 for x in r[:NL - 1]) and _val(r) < 2 * P, op
         if want is None:
-            want = {1: _mont((args[0], args[0])), 4: _val(args[0]) % P}[op]
+            want = {1: lambda: _mont((args[0], args[0])), 4: lambda: _val(args[0]) % P,
+                    11: lambda: (_val(args[0]) - _val(args[1])) % P}[op]()
         assert _val(r) % P == want, op
     # c (canonical affine) enters as the first operand of the madd products
     r = _run_fp(shim, 0, c, S)
@@ -148,8 +153,10 @@ def test_fp2_primitives_at_class_bounds(shim, seed):
     rnd = random.Random(seed) if seed is not None else None
     S2 = _maxlimb(fb.S(), rnd) + _maxlimb(fb.S(), rnd)
     lazy2 = _maxlimb(fb.sub(fb.S(), fb.S()), rnd) + _maxlimb(fb.sub(fb.S(), fb.S()), rnd)
+    # P = U2 - X1 with X1 in class X: < 18p, the widest square input
+    lazy18 = _maxlimb(fb.sub(fb.S(), fb.Xc(), 16), rnd) + _maxlimb(fb.sub(fb.S(), fb.Xc(), 16), rnd)
     shim.h_overflow(1)
-    for op, a, b in ((0, lazy2, lazy2), (1, lazy2, lazy2), (2, lazy2, S2)):
+    for op, a, b in ((0, lazy2, lazy2), (1, lazy2, lazy2), (2, lazy2, S2), (1, lazy18, lazy18), (2, lazy18, S2)):
         r = (ctypes.c_uint32 * (2 * NL))()
         shim.h_fp2_op(op, r, _arr(a), _arr(b), None, None)
         assert shim.h_overflow(1) == 0, op
@@ -244,10 +251,10 @@ def _dec(g, words):
     return (_val(words[:NL]) % P, _val(words[NL:]) % P)
 
 
-def _check_S(g, words):
+def _check_S(g, words, bound=2):
     for k in range(g):
         w = words[k * NL:(k + 1) * NL]
-        assert all(x <= M28 for x in w[:NL - 1]) and _val(w) < 2 * P
+        assert all(x <= M28 for x in w[:NL - 1]) and _val(w) < bound * P
 
 
 @pytest.mark.parametrize("group", [1, 2])
@@ -259,9 +266,11 @@ def test_xyzz_formulas_at_class_bounds(shim, group, seed):
     # seed None: x at the exact class maximum, the other coordinates near it (equal
     # coordinates everywhere would make P = 0, the doubling/infinity branch)
     r2 = rnd or random.Random(98)
-    acc = [_elem(group, rnd, fb.S())] + [_elem(group, r2, fb.S()) for _ in range(3)]
+    # x in class X (normalized, < 10p: the stored x is not reduced), the rest in S
+    acc = [_elem(group, rnd, fb.Xc())] + [_elem(group, r2, fb.S()) for _ in range(3)]
     # (the second operand of the add must differ from acc, else the doubling branch runs)
-    oth = [_elem(group, rnd or random.Random(99), fb.S()) for _ in range(4)]
+    r3 = rnd or random.Random(99)
+    oth = [_elem(group, r3, fb.Xc())] + [_elem(group, r3, fb.S()) for _ in range(3)]
     pt = [_elem(group, rnd, fb.canonical()) for _ in range(2)]
     dec = lambda ws: tuple(_dec(group, w) for w in ws)  # noqa: E731
     shim.h_overflow(1)
@@ -272,7 +281,8 @@ def test_xyzz_formulas_at_class_bounds(shim, group, seed):
         assert shim.h_overflow(1) == 0, (op, neg)
         out = list(a)
         coords = [out[k * W:(k + 1) * W] for k in range(4)]
-        for c in coords:
+        _check_S(group, coords[0], 10)
+        for c in coords[1:]:
             _check_S(group, c)
         if op == 0:
             want = _ref_madd(F, dec(acc), dec(pt), neg)

@@ -147,13 +147,14 @@ def test_mult_batch_matches_single(m, golden):
 @pytest.mark.parametrize("group,log_n,K", [(1, 16, 7), (2, 10, 7), (1, 12, 9), (1, 12, 17), (2, 10, 9),
                                            (2, 10, 17)])
 def test_mult_batch_sets_resident_and_pinned(m, group, log_n, K):
-    """Batches longer than every ring (Ches: kFronts = 3 front sets, kBSets = 2
-    bucket sets, kSlots = 4 device scalar slots whose copies run on their own
-    copy stream): K distinct sets from device memory and from page-locked host
-    memory (streamed set by set inside the pipeline) equal the synchronous MSMs.
-    K = 9 and 17 exceed one reduction group (kGroup = 8): several groups of
-    uneven size R alternate between the two reducer buffer sets / tail streams
-    and read back at their own offsets."""
+    """Batches longer than every ring (Ches: front groups of kFrontGroup = 8 MSMs,
+    the first of one, in kFronts = 2 alternating front sets; kBSets = 2 bucket
+    sets; host sets in 2 x 8 device slots copied on their own stream): K distinct
+    sets from device memory and from page-locked host memory (streamed group by
+    group inside the pipeline) equal the synchronous MSMs.  K = 9 and 17 also
+    exceed one reduction group (kGroup = 8): several groups of uneven size R
+    alternate between the two reducer buffer sets / tail streams and read back
+    at their own offsets, and the front groups (1 + 8 + 8) straddle them."""
     import numpy as np
     import torch
     n = 1 << log_n
