@@ -14,7 +14,8 @@
  * caller serialises).  Errors: the blst-named functions keep blst's void
  * signatures; by default a HIP failure inside one prints the error and aborts
  * (a silent wrong answer is never returned); after msm_set_abort_on_error(0)
- * such a call returns with its result set to the all-zero point (infinity),
+ * such a call returns with its result set to the all-zero point (infinity;
+ * blst_p{1,2}s_mult_wbits_precompute: the whole table zeroed, never half written),
  * msm_error_pending() nonzero and the message in msm_last_error().  The msm_*
  * extension API returns MSM_OK or a negative MSM_E* code and msm_last_error()
  * describes it.

@@ -81,12 +81,13 @@ def lib():
         f.argtypes, f.restype = [vp, sz, vp, sz], None
         f = getattr(L, f"blst_p{g}s_mult_wbits")
         f.argtypes, f.restype = [vp, vp, sz, sz, vp, sz, vp], None
-    L.msm_release_engine_cache.argtypes = []
-    L.msm_release_engine_cache.restype = None
-    L.msm_engine_cache_stats.argtypes = [vp]
-    L.msm_engine_cache_stats.restype = None
-    L.msm_set_engine_cache_limit.argtypes = [sz]
-    L.msm_set_engine_cache_limit.restype = sz
+    if hasattr(L, "msm_release_engine_cache"):  # (absent from older builds used in A/B runs)
+        L.msm_release_engine_cache.argtypes = []
+        L.msm_release_engine_cache.restype = None
+        L.msm_engine_cache_stats.argtypes = [vp]
+        L.msm_engine_cache_stats.restype = None
+        L.msm_set_engine_cache_limit.argtypes = [sz]
+        L.msm_set_engine_cache_limit.restype = sz
     L.msm_set_abort_on_error.argtypes = [i32]
     L.msm_error_pending.argtypes = []
     L.msm_wbits_ctx_create.argtypes = [pp, i32, i32, i32]

@@ -608,7 +608,8 @@ MSM_POINTS_ADD(2)
     try {                                                                                                         \
       wbits_precompute<g>(table, wbits, (const void *const *)points, npoints);                                    \
     } catch (const std::exception &e) {                                                                           \
-      die("blst_p" #g "s_mult_wbits_precompute", e);                                                              \
+      die("blst_p" #g "s_mult_wbits_precompute", e, table,                                                        \
+          blst_p##g##s_mult_wbits_precompute_sizeof(wbits, npoints)); /* no half-written table */                \
     }                                                                                                             \
   }                                                                                                               \
   size_t blst_p##g##s_mult_wbits_scratch_sizeof(size_t npoints) {                                                \
@@ -806,8 +807,14 @@ int msm_ches_ctx_shards(const msm_ches_ctx *ctx) {
 
 #define CHES_DISPATCH(ctx, CALL) ((ctx)->group == 1 ? (ctx)->g1->CALL : (ctx)->g2->CALL)
 
+// several shards take host memory only (each device gets its own slice)
+static bool multi_device_arg(const msm_ches_ctx *ctx, int on_device) {
+  return on_device && (ctx->group == 1 ? ctx->g1->nshards() : ctx->g2->nshards()) > 1;
+}
+
 int msm_ches_ctx_build_table(msm_ches_ctx *ctx, const void *pts, size_t n, int on_device, void *stream) {
   if (!ctx || (!pts && n)) return fail(MSM_E_ARG, "bad args");
+  if (multi_device_arg(ctx, on_device)) return fail(MSM_E_ARG, "a multi-device context takes host points");
   try {
     ctx->ready = false;
     CHES_DISPATCH(ctx, build_table(pts, n, on_device != 0, (hipStream_t)stream));
@@ -820,6 +827,7 @@ int msm_ches_ctx_build_table(msm_ches_ctx *ctx, const void *pts, size_t n, int o
 
 int msm_ches_ctx_set_table(msm_ches_ctx *ctx, const void *tab, size_t n, int on_device, void *stream) {
   if (!ctx || (!tab && n)) return fail(MSM_E_ARG, "bad args");
+  if (multi_device_arg(ctx, on_device)) return fail(MSM_E_ARG, "a multi-device context takes a host table");
   try {
     ctx->ready = false;
     CHES_DISPATCH(ctx, set_table(tab, n, on_device != 0, (hipStream_t)stream));
@@ -844,6 +852,7 @@ int msm_ches_ctx_mult(msm_ches_ctx *ctx, void *ret, const byte *scalars, size_t 
                       void *stream) {
   if (!ctx || !ret || stride < 32) return fail(MSM_E_ARG, "bad args (stride must be >= 32)");
   if (!ctx->ready) return fail(MSM_E_STATE, "no table: build_table, set_table or load_table first");
+  if (multi_device_arg(ctx, on_device)) return fail(MSM_E_ARG, "a multi-device context takes host scalars");
   try {
     DeviceGuard g(ctx->device);
     hipStream_t s = (hipStream_t)stream;
@@ -866,6 +875,7 @@ int msm_ches_ctx_mult_batch(msm_ches_ctx *ctx, void *rets, const byte *scalars, 
                             size_t count, int on_device, void *stream) {
   if (!ctx || (!rets && count) || stride < 32) return fail(MSM_E_ARG, "bad args (stride must be >= 32)");
   if (!ctx->ready) return fail(MSM_E_STATE, "no table: build_table, set_table or load_table first");
+  if (multi_device_arg(ctx, on_device)) return fail(MSM_E_ARG, "a multi-device context takes host scalars");
   try {
     DeviceGuard g(ctx->device);
     hipStream_t s = (hipStream_t)stream;

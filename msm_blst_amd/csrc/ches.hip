@@ -129,6 +129,21 @@ void ches_digit_code(const std::vector<int> &B, int q, std::vector<uint32_t> &co
 }
 #endif  // MSM_GROUP == 1
 
+// a tail level of segment sums: few outputs are latency-bound, so one add
+// spreads over 4 waves (coop.hpp: G1 one lane per wave, G2 a lane pair per wave)
+template <int G>
+static void launch_segsum_tail(hipStream_t s, const Xyzz<typename FieldOf<G>::F> *src, const uint32_t *ix,
+                               const uint32_t *st, Xyzz<typename FieldOf<G>::F> *dst, size_t nout, bool coop) {
+  if (coop && nout <= 16384) {
+    if constexpr (G == 1)
+      hipLaunchKernelGGL(k_segsum_c<G>, dim3(nblk(nout, 64)), dim3(256), 0, s, src, ix, st, dst, nout);
+    else
+      hipLaunchKernelGGL(k_segsum_c2p, dim3(nblk(nout, 32)), dim3(256), 0, s, src, ix, st, dst, nout);
+  } else {
+    launch_segsum<G>(s, src, ix, st, dst, nout);
+  }
+}
+
 // -------------------------------------------------------------- scan reduce --
 template <int G>
 void ScanReducer<G>::launch(hipStream_t s, const void *Abuf, int W, int S, bool coop) {
@@ -142,7 +157,10 @@ void ScanReducer<G>::launch(hipStream_t s, const void *Abuf, int W, int S, bool 
   int cur = 0;
   for (int d = 1; d < S; d <<= 1) {  // suffix sums T_k = sum_{b >= k} A_b
     Xyzz<F> *dst = buf[cur].as<Xyzz<F>>();
-    if (G == 2)  // lane pairs (fp2l.hpp)
+    if (G == 2 && coop)  // lane pairs (fp2l.hpp), one add over 4 waves (coop.hpp)
+      hipLaunchKernelGGL(k_suffix_step_c2p, dim3(nblk(NT, 32)), dim3(256), 0, s,
+                         reinterpret_cast<const Xyzz<Fp2> *>(src), reinterpret_cast<Xyzz<Fp2> *>(dst), S, d, W);
+    else if (G == 2)  // lane pairs (fp2l.hpp)
       hipLaunchKernelGGL(k_suffix_step2p, dim3(nblk(2 * NT, 64)), dim3(64), 0, s,
                          reinterpret_cast<const Xyzz<Fp2> *>(src), reinterpret_cast<Xyzz<Fp2> *>(dst), S, d, W);
     else if (coop) hipLaunchKernelGGL(k_suffix_step_c<G>, dim3(nblk(NT, 64)), dim3(256), 0, s, src, dst, S, d, W);
@@ -153,7 +171,10 @@ void ScanReducer<G>::launch(hipStream_t s, const void *Abuf, int W, int S, bool 
   }
   for (size_t len = NT; len > (size_t)W; len >>= 1) {  // sum_k T_k = sum_b b A_b
     Xyzz<F> *dst = buf[cur].as<Xyzz<F>>();
-    if (G == 2)
+    if (G == 2 && coop)
+      hipLaunchKernelGGL(k_pair_step_c2p, dim3(nblk(len / 2, 32)), dim3(256), 0, s,
+                         reinterpret_cast<const Xyzz<Fp2> *>(src), reinterpret_cast<Xyzz<Fp2> *>(dst), len / 2);
+    else if (G == 2)
       hipLaunchKernelGGL(k_pair_step2p, dim3(nblk(len, 64)), dim3(64), 0, s,
                          reinterpret_cast<const Xyzz<Fp2> *>(src), reinterpret_cast<Xyzz<Fp2> *>(dst), len / 2);
     else if (coop) hipLaunchKernelGGL(k_pair_step_c<G>, dim3(nblk(len / 2, 64)), dim3(256), 0, s, src, dst, len / 2);
@@ -249,7 +270,7 @@ void WeightedReducer<G>::plan(const std::vector<uint32_t> &w, const std::vector<
       for (size_t q = 0; q < cur_seg.size(); ++q)
         if (cur_seg[q] / S == blk && (((cur_seg[q] % S) + 1) >> j & 1u)) bidx.push_back((uint32_t)q), bseg.push_back(bs);
     }
-    int Cb = 8;
+    int Cb = 2;  // pairwise from the first level: the tail is latency-bound (a chunk of 8 is 7 serial adds in one lane)
     while (!bseg.empty()) {
       std::vector<uint32_t> st, nseg;
       size_t k = 0;
@@ -351,10 +372,7 @@ void WeightedReducer<G>::launch_tail(hipStream_t s, int set, bool coop) {
     int cur = 0;
     auto segsum = [&](const Xyzz<F> *a, const uint32_t *ix, const uint32_t *st, Xyzz<F> *d, size_t nout) {
       if (!nout) return;
-      if (G == 1 && coop && nout <= 16384)
-        hipLaunchKernelGGL(k_segsum_c<G>, dim3(nblk(nout, 64)), dim3(256), 0, s, a, ix, st, d, nout);
-      else
-        launch_segsum<G>(s, a, ix, st, d, nout);
+      launch_segsum_tail<G>(s, a, ix, st, d, nout, coop);
       MSM_HIP_CHECK(hipGetLastError());
     };
     for (size_t l = 1; l + 1 < L; ++l) {
@@ -381,13 +399,7 @@ void WeightedReducer<G>::launch_tail(hipStream_t s, int set, bool coop) {
     const bool last = l + 1 == L;
     Xyzz<F> *dst = last ? dense_buf_[set].as<Xyzz<F>>() : part_[set][l & 1].as<Xyzz<F>>();
     const uint32_t *ix = last ? idx_.as<uint32_t>() + final_perm_off_ : nullptr;
-    if (nout_[l]) {
-      if (G == 1 && coop && nout_[l] <= 16384)  // few outputs: latency-bound, 4 waves per add
-        hipLaunchKernelGGL(k_segsum_c<G>, dim3(nblk(nout_[l], 64)), dim3(256), 0, s, src, ix,
-                           starts_[l].as<uint32_t>(), dst, nout_[l]);
-      else  // G2: lane pairs (fp2l.hpp) at every level
-        launch_segsum<G>(s, src, ix, starts_[l].as<uint32_t>(), dst, nout_[l]);
-    }
+    if (nout_[l]) launch_segsum_tail<G>(s, src, ix, starts_[l].as<uint32_t>(), dst, nout_[l], coop);
     MSM_HIP_CHECK(hipGetLastError());
     src = dst;
   }
@@ -739,10 +751,19 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
     MSM_HIP_CHECK(hipHostMalloc(&host_out_, bytes, hipHostMallocDefault));
     host_out_bytes_ = bytes;
   }
-  // front groups: [0, 1), then up to kFrontGroup MSMs each.  The first group is a
-  // single MSM so the first accumulation starts after one front, not eight.
+  // (group size cap: kFrontGroupDefault, or MSM_FRONT_GROUP=<1..8>; engine.hpp)
+  static const size_t fg_max = [] {
+    const char *e = getenv("MSM_FRONT_GROUP");
+    return (size_t)std::min(kFrontGroup, std::max(1, e ? atoi(e) : kFrontGroupDefault));
+  }();
+  // front groups of 1, 1, 2, 4, then fg_max MSMs: the first accumulation
+  // starts after one front, and each group's host sets (copied while the earlier
+  // groups accumulate: a set copies in ~0.6 ms, an MSM accumulates in ~2.3) are
+  // in HBM before its front is due -- a first group of eight stalled the H2D
+  // batch by ~5 ms (the 256-MiB copy, then the front, before MSM 1).
   std::vector<size_t> fgb{0};
-  while (fgb.back() < count) fgb.push_back(std::min(count, fgb.back() == 0 ? (size_t)1 : fgb.back() + kFrontGroup));
+  while (fgb.back() < count)
+    fgb.push_back(std::min(count, fgb.back() + std::min<size_t>(fg_max, std::max<size_t>(1, fgb.back()))));
   const size_t nfg = fgb.size() - 1;
   // every buffer the loop touches exists before the first launch (an allocation
   // inside the issue loop could synchronise the device)
@@ -752,16 +773,16 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
   // reallocate (a hipFree inside the pipelined region would synchronise it)
   for (int t = 0; t < kBSets && (size_t)t < ngroups; ++t) red_.ensure_group(t, kGroup);
   // front sets sized for a whole front group (the sort's scan scratch too): run
-  // one sort of kFrontGroup sets per set before the loop if they are not yet
-  // sized (kFrontGroup dummy sets of all-zero scalars, outside the batch timing)
+  // one sort of fg_max sets per set before the loop if they are not yet sized
+  // (fg_max dummy sets of all-zero scalars, outside the batch timing)
   const size_t sslot = n * stride;  // one device scalar slot
-  if (scalars_on_host || fs_[0].sorted.bytes < n * (size_t)p_.h * kFrontGroup * 4) {
-    scal_.ensure(2 * kFrontGroup * sslot + 16);
-  }
+  bool unsized = false;
+  for (int f = 0; f < kFronts && (size_t)f < nfg; ++f) unsized |= fs_[f].sorted.bytes < n * (size_t)p_.h * fg_max * 4;
+  if (scalars_on_host || unsized) scal_.ensure(2 * fg_max * sslot + 16);
   for (int f = 0; f < kFronts && (size_t)f < nfg; ++f)
-    if (fs_[f].sorted.bytes < n * (size_t)p_.h * kFrontGroup * 4) {
-      MSM_HIP_CHECK(hipMemsetAsync(scal_.p, 0, kFrontGroup * sslot, s));
-      digits_sort(s, scal_.as<uint8_t>(), stride, sslot, kFrontGroup, f);
+    if (fs_[f].sorted.bytes < n * (size_t)p_.h * fg_max * 4) {
+      MSM_HIP_CHECK(hipMemsetAsync(scal_.p, 0, fg_max * sslot, s));
+      digits_sort(s, scal_.as<uint8_t>(), stride, sslot, (int)fg_max, f);
       MSM_HIP_CHECK(hipStreamSynchronize(s));
     }
   const bool prof = profile_;
@@ -806,7 +827,7 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
   MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, bev_[0], 0));
   MSM_HIP_CHECK(hipStreamWaitEvent(cstream_, bev_[0], 0));
   for (int t = 0; t < kBSets; ++t) MSM_HIP_CHECK(hipStreamWaitEvent(tails_[t], bev_[0], 0));
-  auto slots = [&](size_t g) { return scal_.as<uint8_t>() + (g % 2) * kFrontGroup * sslot; };
+  auto slots = [&](size_t g) { return scal_.as<uint8_t>() + (g % 2) * fg_max * sslot; };
   auto copy_group = [&](size_t g) {
     if (!scalars_on_host || g >= nfg) return;
     if (g >= 2) MSM_HIP_CHECK(hipStreamWaitEvent(cstream_, evf[g - 2], 0));  // slots consumed by front g - 2

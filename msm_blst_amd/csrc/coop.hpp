@@ -14,7 +14,11 @@
 //   L4  ZZZ3        | X3, Y3 = R (Q - X3) - S1 PPP
 // Same formulas and range classes as xyzz_add (ec.hpp); the rare branches
 // (an input at infinity, P == +-bucket) take the serial formulas.
+// G2 runs the same split on lane pairs (fp2l.hpp): F = Fp2L, lanes 2i / 2i+1 of
+// every wave hold the two components of add i, so a 256-thread workgroup does
+// 32 G2 adds with 8 lanes each (the *_c2p kernels below).
 #pragma once
+#include "fp2l.hpp"
 #include "kernels.hpp"
 
 namespace msm {
@@ -29,6 +33,8 @@ __device__ __forceinline__ uint32_t &fw(Fp &x, int k) { return x.v[k]; }
 __device__ __forceinline__ uint32_t fw(const Fp &x, int k) { return x.v[k]; }
 __device__ __forceinline__ uint32_t &fw(Fp2 &x, int k) { return k < NL ? x.c0.v[k] : x.c1.v[k - NL]; }
 __device__ __forceinline__ uint32_t fw(const Fp2 &x, int k) { return k < NL ? x.c0.v[k] : x.c1.v[k - NL]; }
+__device__ __forceinline__ uint32_t &fw(Fp2L &x, int k) { return x.c.v[k]; }
+__device__ __forceinline__ uint32_t fw(const Fp2L &x, int k) { return x.c.v[k]; }
 
 template <class F>
 __device__ __forceinline__ void coop_put(CoopLds<F> &L, int slot, int lane, const F &x) {
@@ -63,12 +69,13 @@ __device__ __forceinline__ F fsel4(int w, const F &x0, const F &x1, const F &x2,
   return r;
 }
 
-// *dst = a + b.  Every thread of the 256-thread workgroup calls this with the
-// (a, b, dst, active) of its lane (the 4 waves pass the same values); it
-// contains three __syncthreads.  The operands of each level are selected by
-// value per wave so that every wave runs the same product code.
-template <class F>
-__device__ __forceinline__ void coop_xyzz_add(const Xyzz<F> &a, const Xyzz<F> &b, Xyzz<F> *dst, bool active,
+// a + b -> st(coordinate, value) (coordinate: 0 x, 1 y, 2 zzz, 3 zz).  Every
+// thread of the 256-thread workgroup calls this with the (a, b, active) of its
+// lane (the 4 waves pass the same values); it contains three __syncthreads.
+// The operands of each level are selected by value per wave so that every wave
+// runs the same product code.
+template <class F, class Store>
+__device__ __forceinline__ void coop_xyzz_add(const Xyzz<F> &a, const Xyzz<F> &b, Store st, bool active,
                                               CoopLds<F> &L) {
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   F r;
@@ -123,8 +130,36 @@ __device__ __forceinline__ void coop_xyzz_add(const Xyzz<F> &a, const Xyzz<F> &b
     o0 = fsel4(w, b.zzz, b.x, b.zz, b.zz);
     o1 = b.y;
   }
-  if (w < 3) coop_st(dst, w == 0 ? 2 : w == 1 ? 0 : 3, o0);
-  if (w == 1) coop_st(dst, 1, o1);
+  if (w < 3) st(w == 0 ? 2 : w == 1 ? 0 : 3, o0);
+  if (w == 1) st(1, o1);
+}
+template <class F>
+__device__ __forceinline__ void coop_xyzz_add(const Xyzz<F> &a, const Xyzz<F> &b, Xyzz<F> *dst, bool active,
+                                              CoopLds<F> &L) {
+  coop_xyzz_add(a, b, [&](int c, const F &v) { coop_st(dst, c, v); }, active, L);
+}
+// G2 lane pairs: this lane's component of coordinate c goes to dst
+__device__ __forceinline__ void coop_st2l(Xyzz<Fp2> *dst, int c, const Fp2L &v) {
+  Fp2 *p = c == 0 ? &dst->x : c == 1 ? &dst->y : c == 2 ? &dst->zzz : &dst->zz;
+  const int comp = (int)(threadIdx.x & 1);
+  uint2 *d = reinterpret_cast<uint2 *>(reinterpret_cast<uint8_t *>(p) + comp * sizeof(Fp));
+#pragma unroll
+  for (int i = 0; i < NL / 2; ++i) d[i] = make_uint2(v.c.v[2 * i], v.c.v[2 * i + 1]);
+}
+__device__ __forceinline__ void coop_ld2l(Xyzz<Fp2L> &r, const Xyzz<Fp2> *p) {
+  const int comp = (int)(threadIdx.x & 1);
+  const Fp2 *f[4] = {&p->x, &p->y, &p->zzz, &p->zz};
+  Fp *o[4] = {&r.x.c, &r.y.c, &r.zzz.c, &r.zz.c};
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const uint2 *s = reinterpret_cast<const uint2 *>(reinterpret_cast<const uint8_t *>(f[c]) + comp * sizeof(Fp));
+#pragma unroll
+    for (int i = 0; i < NL / 2; ++i) {
+      const uint2 v = s[i];
+      o[c]->v[2 * i] = v.x;
+      o[c]->v[2 * i + 1] = v.y;
+    }
+  }
 }
 
 // ---- tail-level kernels: 256 threads = 4 waves per 64 outputs ----
@@ -188,6 +223,64 @@ static __global__ void __launch_bounds__(256)
     }
   }
   coop_xyzz_add(a, b, &dst[active ? t : 0], active, L);
+}
+
+// ---- G2: the same kernels on lane pairs, 256 threads = 4 waves per 32 outputs ----
+__device__ __forceinline__ Xyzz<Fp2L> coop_inf2l() {
+  Xyzz<Fp2L> z;
+  xyzz_set_inf(z);
+  return z;
+}
+
+static __global__ void __launch_bounds__(256)
+    k_pair_step_c2p(const Xyzz<Fp2> *__restrict__ in, Xyzz<Fp2> *__restrict__ out, size_t nout) {
+  __shared__ CoopLds<Fp2L> L;
+  const size_t t = (size_t)blockIdx.x * 32 + ((threadIdx.x & 63) >> 1);
+  const bool active = t < nout;
+  Xyzz<Fp2L> a = coop_inf2l(), b = coop_inf2l();
+  if (active) {
+    coop_ld2l(a, &in[2 * t]);
+    coop_ld2l(b, &in[2 * t + 1]);
+  }
+  Xyzz<Fp2> *d = &out[active ? t : 0];
+  coop_xyzz_add(a, b, [&](int c, const Fp2L &v) { coop_st2l(d, c, v); }, active, L);
+}
+
+static __global__ void __launch_bounds__(256)
+    k_suffix_step_c2p(const Xyzz<Fp2> *__restrict__ in, Xyzz<Fp2> *__restrict__ out, int S, int dd, int W) {
+  __shared__ CoopLds<Fp2L> L;
+  const size_t t = (size_t)blockIdx.x * 32 + ((threadIdx.x & 63) >> 1);
+  const bool active = t < (size_t)W * S;
+  const int k = active ? (int)(t % (size_t)S) : 0;
+  Xyzz<Fp2L> a = coop_inf2l(), b = coop_inf2l();
+  if (active) coop_ld2l(a, &in[t]);
+  if (active && k + dd < S) coop_ld2l(b, &in[t + dd]);
+  Xyzz<Fp2> *d = &out[active ? t : 0];
+  coop_xyzz_add(a, b, [&](int c, const Fp2L &v) { coop_st2l(d, c, v); }, active, L);
+}
+
+// segment sums as k_segsum_c, for G2 on lane pairs
+static __global__ void __launch_bounds__(256)
+    k_segsum_c2p(const Xyzz<Fp2> *__restrict__ src, const uint32_t *__restrict__ idx,
+                 const uint32_t *__restrict__ starts, Xyzz<Fp2> *__restrict__ dst, size_t nout) {
+  __shared__ CoopLds<Fp2L> L;
+  const size_t t = (size_t)blockIdx.x * 32 + ((threadIdx.x & 63) >> 1);
+  const bool active = t < nout;
+  Xyzz<Fp2L> a = coop_inf2l(), b = coop_inf2l();
+  if (active) {
+    const uint32_t lo = starts[t], hi = starts[t + 1];
+    if (hi > lo) {
+      coop_ld2l(a, &src[idx ? idx[lo] : lo]);
+      for (uint32_t k = lo + 1; k + 1 < hi; ++k) {
+        Xyzz<Fp2L> c;
+        coop_ld2l(c, &src[idx ? idx[k] : k]);
+        xyzz_add(a, c);
+      }
+      if (hi - lo >= 2) coop_ld2l(b, &src[idx ? idx[hi - 1] : hi - 1]);
+    }
+  }
+  Xyzz<Fp2> *d = &dst[active ? t : 0];
+  coop_xyzz_add(a, b, [&](int c, const Fp2L &v) { coop_st2l(d, c, v); }, active, L);
 }
 
 }  // namespace msm

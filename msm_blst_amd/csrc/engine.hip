@@ -7,6 +7,7 @@
 
 #include "bucket_sort.hpp"
 #include "engine.hpp"
+#include "hoststage.hpp"
 #include "kernels.hpp"
 #include "pair_kernels.hpp"
 
@@ -204,8 +205,9 @@ void Pippenger<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, i
 }
 
 // The blst drop-in (abi.cpp blst_p{1,2}s_mult_pippenger / _tile_pippenger):
-// points and scalars in the caller's host memory.  The scalars go up first and
-// their digits + sort are enqueued; the 96 n G bytes of points then upload (and
+// points and scalars in the caller's host memory, uploaded through the
+// engine's pinned ring (hoststage.hpp).  The scalars go up first and their
+// digits + sort are enqueued; the 96 n G bytes of points then upload (and
 // convert) on a second stream while the GPU sorts, and the accumulation waits
 // for them.  tile != nullptr: one blst window tile -- k_tile_booth turns the
 // raw scalars into |Booth digit| + sign on the device, and the plain pipeline
@@ -227,9 +229,10 @@ void Pippenger<G>::run_host(hipStream_t s, const void *pts_blst, size_t n, const
     MSM_HIP_CHECK(hipEventCreateWithFlags(&ev_up_, hipEventDisableTiming));
     MSM_HIP_CHECK(hipEventCreateWithFlags(&ev_s_, hipEventDisableTiming));
   }
+  if (!stage_) stage_ = std::make_unique<HostStager>();
   const size_t sbytes = n * stride;
   scal_.ensure(sbytes + (tile ? n * 5 : 0) + 16);
-  MSM_HIP_CHECK(hipMemcpyAsync(scal_.p, scalars, sbytes, hipMemcpyHostToDevice, s));
+  stage_->upload(scal_.p, scalars, sbytes, s);
   if (tile) {
     uint32_t *mag = reinterpret_cast<uint32_t *>(scal_.as<uint8_t>() + ((sbytes + 3) & ~(size_t)3));
     uint8_t *neg = reinterpret_cast<uint8_t *>(mag + n);
@@ -247,7 +250,7 @@ void Pippenger<G>::run_host(hipStream_t s, const void *pts_blst, size_t n, const
   const size_t raw = n * 96 * G;
   tmp_.ensure(raw);
   pts_.ensure(n * sizeof(Aff<F>));
-  MSM_HIP_CHECK(hipMemcpyAsync(tmp_.p, pts_blst, raw, hipMemcpyHostToDevice, up_));
+  stage_->upload(tmp_.p, pts_blst, raw, up_);
   hipLaunchKernelGGL(k_convert_points<G>, dim3(nblk(n, 256)), dim3(256), 0, up_, tmp_.as<uint64_t>(),
                      pts_.as<Aff<F>>(), n);
   MSM_HIP_CHECK(hipGetLastError());

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -18,6 +19,8 @@
   } while (0)
 
 namespace msm {
+
+class HostStager;  // hoststage.hpp: pinned-ring uploads from pageable caller memory
 
 inline unsigned nblk(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
 
@@ -238,6 +241,7 @@ class Pippenger {
   bool profile_ = false;
   PhaseTimes times_;
   DevBuf pts_, keys_, vals_, counts_, offsets_, sorted_, order_, buckets_, tmp_, scal_;
+  std::unique_ptr<HostStager> stage_;  // run_host: uploads from the caller's pageable memory
   hipStream_t up_ = nullptr;  // run_host: point upload stream
   hipEvent_t ev_up_ = nullptr, ev_s_ = nullptr;
   // digits + sort; neg: optional per-point sign flips (tiles)
@@ -314,14 +318,18 @@ class Ches {
   // MSM k-1 still reads the other one
   static constexpr int kBSets = 2;
   DevBuf code_, rank_, table_, buckets_[kBSets];
-  // digit/sort outputs.  A batch runs the fronts (digits + sort, memory/LDS-
-  // bound) of up to kFrontGroup MSMs in ONE pass per stage (seven launches for
-  // the group instead of seven per MSM: every launch beside an accumulation
-  // costs it ~10-20 us), front group g+1 beside group g's accumulations; two
-  // front sets alternate between the groups.  The synchronous MSM uses set 0
-  // with one scalar set.
+  // digit/sort outputs.  A batch can run the fronts (digits + sort) of up to
+  // kFrontGroup MSMs in ONE pass per stage (seven launches for the group instead
+  // of seven per MSM), front group g+1 beside group g's accumulations, two front
+  // sets alternating.  Measured on MI355X (tools/ab_env.sh, profiles/
+  // r03_front_group_ab.txt) the grouped fronts slow the accumulations they run
+  // beside more than the launches they save (resident 2.33-2.38 ms per MSM with
+  // groups of 8 vs 2.26-2.27 with groups of 1), so the default group is one
+  // MSM; MSM_FRONT_GROUP=<2..8> selects larger groups.  The synchronous MSM uses
+  // set 0 with one scalar set.
   static constexpr int kGroup = 8;       // batch: MSMs per reduction group (WeightedReducer::launch_tail_group)
-  static constexpr int kFrontGroup = 8;  // batch: MSMs per front group (the first group holds one MSM)
+  static constexpr int kFrontGroup = 8;  // batch: largest front group (ramping up 1, 1, 2, 4, 8)
+  static constexpr int kFrontGroupDefault = 1;
   static constexpr int kFronts = 2;
   ChesFrontSet fs_[kFronts];
   // host scalar sets of a batch: two groups of kFrontGroup device slots, copied on

@@ -1,0 +1,197 @@
+// hoststage.hpp -- uploads from caller-owned pageable host memory.
+//
+// The blst entry points receive points and scalars in the caller's memory
+// (ref multi_scalar.c:581-607), usually fresh pageable buffers.  HIP's own
+// pageable copy path pins user pages on the fly: measured on MI355X it is as
+// fast as a pinned copy for a buffer it has seen before (56 GB/s for 128 MiB),
+// but 10-37 ms per 2^20-point call with fresh buffers, growing call by call
+// (tools/dropin_timing.py).  HostStager instead streams the bytes through a
+// small pinned ring: the host copy of chunk c + 1 (split over a persistent
+// worker pool) overlaps the DMA of chunk c, so the upload runs at the DMA rate
+// (tools/microbench/h2d_stage.cpp: 16 MiB x 4 slots, 4-8 threads ~49 GB/s).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <exception>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "engine.hpp"
+
+namespace msm {
+
+// Process-wide pool of host worker threads (never destroyed: the workers park
+// on a condition variable for the life of the process).  parallel_for runs
+// f(0..n-1) on the workers and the calling thread and returns when all are
+// done; concurrent callers take turns.
+class WorkerPool {
+ public:
+  static WorkerPool &get() {
+    static WorkerPool *p = new WorkerPool();
+    return *p;
+  }
+  size_t size() const { return th_.size() + 1; }
+
+  void parallel_for(size_t n, const std::function<void(size_t)> &f) {
+    if (n == 0) return;
+    if (n == 1 || th_.empty()) {
+      for (size_t i = 0; i < n; ++i) f(i);
+      return;
+    }
+    std::lock_guard<std::mutex> turn(call_mu_);
+    auto job = std::make_shared<Job>();
+    job->f = &f;
+    job->n = n;
+    job->remaining = n;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      job_ = job;
+      ++gen_;
+    }
+    cv_.notify_all();
+    run(*job);
+    {
+      std::unique_lock<std::mutex> lk(job->mu);
+      job->done.wait(lk, [&] { return job->remaining == 0; });
+    }
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      job_.reset();
+    }
+    if (job->err) std::rethrow_exception(job->err);
+  }
+
+ private:
+  struct Job {
+    const std::function<void(size_t)> *f = nullptr;
+    size_t n = 0;
+    std::atomic<size_t> next{0};
+    size_t remaining = 0;  // guarded by mu
+    std::exception_ptr err;
+    std::mutex mu;
+    std::condition_variable done;
+  };
+  std::mutex call_mu_, mu_;
+  std::condition_variable cv_;
+  std::shared_ptr<Job> job_;
+  uint64_t gen_ = 0;
+  std::vector<std::thread> th_;
+
+  WorkerPool() {
+    // the box's CPU share per GPU is 16 threads; host copies saturate at ~8
+    // (h2d_stage: 142 GB/s memcpy into pinned memory with 8 threads)
+    size_t want = 7;
+    if (const char *e = getenv("MSM_HOST_THREADS")) want = (size_t)std::max(1, atoi(e)) - 1;
+    const size_t hw = std::thread::hardware_concurrency();
+    if (hw) want = std::min(want, hw > 1 ? hw - 1 : 0);
+    for (size_t t = 0; t < want; ++t) th_.emplace_back([this] { loop(); });
+    for (auto &t : th_) t.detach();
+  }
+  static void run(Job &j) {
+    size_t i;
+    while ((i = j.next.fetch_add(1)) < j.n) {
+      try {
+        (*j.f)(i);
+      } catch (...) {
+        std::lock_guard<std::mutex> g(j.mu);
+        if (!j.err) j.err = std::current_exception();
+      }
+      std::lock_guard<std::mutex> g(j.mu);
+      if (--j.remaining == 0) j.done.notify_all();
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      std::shared_ptr<Job> j;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        j = job_;
+      }
+      if (j) run(*j);  // a stale job has next >= n: nothing to do
+    }
+  }
+};
+
+// memcpy of `bytes` split over the worker pool (1-MiB pieces or more)
+inline void parallel_memcpy(void *dst, const void *src, size_t bytes) {
+  const size_t piece = std::max<size_t>((size_t)1 << 20, (bytes + 7) / 8);
+  const size_t n = (bytes + piece - 1) / piece;
+  WorkerPool::get().parallel_for(n, [&](size_t i) {
+    const size_t a = i * piece, b = std::min(bytes, a + piece);
+    memcpy(static_cast<uint8_t *>(dst) + a, static_cast<const uint8_t *>(src) + a, b - a);
+  });
+}
+
+// true if p is page-locked / registered host memory (a direct DMA source)
+inline bool host_pinned(const void *p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();  // unregistered pageable memory reports an error: clear it
+    return false;
+  }
+  return a.type == hipMemoryTypeHost || a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
+}
+
+// Pinned ring for host -> device uploads; one per engine (engines are leased by
+// one thread at a time, pool.hpp).
+class HostStager {
+ public:
+  static constexpr size_t kChunk = (size_t)16 << 20;
+  static constexpr int kSlots = 4;
+  HostStager() = default;
+  HostStager(const HostStager &) = delete;
+  HostStager &operator=(const HostStager &) = delete;
+  ~HostStager() {
+    for (int k = 0; k < kSlots; ++k)
+      if (ev_[k]) {
+        (void)hipEventSynchronize(ev_[k]);
+        (void)hipEventDestroy(ev_[k]);
+      }
+    if (ring_) (void)hipHostFree(ring_);
+  }
+  size_t pinned_bytes() const { return ring_ ? kChunk * kSlots : 0; }
+
+  // dst (device) <- src (host), enqueued on s; returns when every chunk is
+  // enqueued and src is no longer read.  Pinned sources go straight to the DMA.
+  void upload(void *dst, const void *src, size_t bytes, hipStream_t s) {
+    if (!bytes) return;
+    if (host_pinned(src)) {
+      MSM_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
+      return;
+    }
+    if (!ring_) {
+      MSM_HIP_CHECK(hipHostMalloc(&ring_, kChunk * kSlots, hipHostMallocDefault));
+      for (int k = 0; k < kSlots; ++k) MSM_HIP_CHECK(hipEventCreateWithFlags(&ev_[k], hipEventDisableTiming));
+    }
+    for (size_t off = 0; off < bytes; off += kChunk) {
+      const int k = next_;
+      next_ = (next_ + 1) % kSlots;
+      if (used_[k]) MSM_HIP_CHECK(hipEventSynchronize(ev_[k]));  // the slot's previous DMA is done
+      const size_t len = std::min(kChunk, bytes - off);
+      uint8_t *slot = static_cast<uint8_t *>(ring_) + (size_t)k * kChunk;
+      parallel_memcpy(slot, static_cast<const uint8_t *>(src) + off, len);
+      MSM_HIP_CHECK(hipMemcpyAsync(static_cast<uint8_t *>(dst) + off, slot, len, hipMemcpyHostToDevice, s));
+      MSM_HIP_CHECK(hipEventRecord(ev_[k], s));
+      used_[k] = true;
+    }
+  }
+
+ private:
+  void *ring_ = nullptr;
+  hipEvent_t ev_[kSlots] = {};
+  bool used_[kSlots] = {};
+  int next_ = 0;
+};
+
+}  // namespace msm

@@ -10,6 +10,10 @@
 // (one host thread per shard, each driving its own device), and the single
 // exchange is the read-back of the shards' 144/288-B Jacobian partials, folded
 // on the host with an exact add (hfp::addj, doubling aware) in shard order.
+// Each shard has a persistent host worker thread (created with the context; a
+// thread per shard per call was a visible fixed cost at 2^18 points per GPU,
+// where one MSM takes < 1 ms), and host scalars reach each device through the
+// shard's pinned ring (hoststage.hpp) instead of a pageable copy.
 // No device-to-device traffic is needed: the partials reach host memory with
 // the per-MSM read-back every shard does anyway, so a collective (RCCL) would
 // only add a hop for 144 bytes.  The reference itself is single-device; its Go
@@ -19,13 +23,17 @@
 // Shards may share a device (devices = {0, 0, ...}): each engine keeps its own
 // buffers and streams, which is how the 1-GPU tests exercise the 8-shard fold.
 #pragma once
+#include <condition_variable>
 #include <cstring>
 #include <exception>
+#include <functional>
 #include <memory>
+#include <mutex>
 #include <thread>
 #include <vector>
 
 #include "engine.hpp"
+#include "hoststage.hpp"
 
 namespace msm {
 
@@ -38,30 +46,43 @@ class ChesMulti {
     size_t start = 0, n = 0;  // global point range [start, start + n)
     std::unique_ptr<Ches<G>> eng;
     DevBuf scal;               // host scalars of this shard, per call
+    HostStager stage;          // pinned ring for those scalars
     hipStream_t stream = nullptr;  // the shard's own stream (shards may share a device)
+  };
+  // one persistent host thread per shard (several shards): each() hands every
+  // worker the same task and waits for all of them
+  struct Worker {
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::function<void()> task;
+    bool has = false, quit = false, done = false;
+    std::exception_ptr err;
   };
 
   ChesMulti(const std::vector<int> &devices, const ChesParams &p) : p_(p) {
     if (devices.empty()) throw std::runtime_error("ChesMulti: no devices");
-    shards_.resize(devices.size());
-    for (size_t g = 0; g < devices.size(); ++g) {
-      Shard &s = shards_[g];
-      s.device = devices[g];
-      s.eng = std::make_unique<Ches<G>>(s.device, p);
-      if (devices.size() > 1) {
-        DeviceGuard dg(s.device);
-        MSM_HIP_CHECK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+    shards_ = std::vector<Shard>(devices.size());
+    try {
+      for (size_t g = 0; g < devices.size(); ++g) {
+        Shard &s = shards_[g];
+        s.device = devices[g];
+        s.eng = std::make_unique<Ches<G>>(s.device, p);
+        if (devices.size() > 1) {
+          DeviceGuard dg(s.device);
+          MSM_HIP_CHECK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+        }
       }
+      if (devices.size() > 1) {
+        workers_ = std::vector<Worker>(devices.size());
+        for (Worker &w : workers_) w.th = std::thread([&w] { work(w); });
+      }
+    } catch (...) {
+      release();  // the destructor does not run for a constructor that throws
+      throw;
     }
   }
-  ~ChesMulti() {
-    for (Shard &s : shards_)
-      if (s.stream) {
-        DeviceGuard dg(s.device);
-        (void)hipStreamSynchronize(s.stream);
-        (void)hipStreamDestroy(s.stream);
-      }
-  }
+  ~ChesMulti() { release(); }
   ChesMulti(const ChesMulti &) = delete;
   ChesMulti &operator=(const ChesMulti &) = delete;
   size_t nshards() const { return shards_.size(); }
@@ -118,7 +139,7 @@ class ChesMulti {
       if (!on_device && sh.n) {
         DeviceGuard g(sh.device);
         sh.scal.ensure(sh.n * stride + 16);
-        MSM_HIP_CHECK(hipMemcpyAsync(sh.scal.p, scalars, sh.n * stride, hipMemcpyHostToDevice, s));
+        sh.stage.upload(sh.scal.p, scalars, sh.n * stride, s);
         d = static_cast<const uint8_t *>(sh.scal.p);
       }
       sh.eng->run(s, d, stride, out);
@@ -131,8 +152,7 @@ class ChesMulti {
       hfp::Jac<HF> r;
       if (sh.n) {
         sh.scal.ensure(sh.n * stride + 16);
-        MSM_HIP_CHECK(hipMemcpyAsync(sh.scal.p, scalars + sh.start * stride, sh.n * stride, hipMemcpyHostToDevice,
-                                     sh.stream));
+        sh.stage.upload(sh.scal.p, scalars + sh.start * stride, sh.n * stride, sh.stream);
         sh.eng->run(sh.stream, static_cast<const uint8_t *>(sh.scal.p), stride, &r);
       } else {
         std::memset(&r, 0, sizeof r);
@@ -185,22 +205,81 @@ class ChesMulti {
     }
     n_ = n;
   }
-  // run f on every shard, one host thread each; the first exception is rethrown
+  std::vector<Worker> workers_;  // one per shard when there are several
+  std::mutex each_mu_;           // one each() at a time per context
+
+  static void work(Worker &w) {
+    for (;;) {
+      std::function<void()> t;
+      {
+        std::unique_lock<std::mutex> lk(w.mu);
+        w.cv.wait(lk, [&] { return w.has || w.quit; });
+        if (w.quit) return;
+        t = std::move(w.task);
+        w.has = false;
+      }
+      std::exception_ptr err;
+      try {
+        t();
+      } catch (...) {
+        err = std::current_exception();
+      }
+      {
+        std::lock_guard<std::mutex> g(w.mu);
+        w.err = err;
+        w.done = true;
+      }
+      w.cv.notify_all();
+    }
+  }
+  void release() {
+    for (Worker &w : workers_) {
+      {
+        std::lock_guard<std::mutex> g(w.mu);
+        w.quit = true;
+      }
+      w.cv.notify_all();
+      if (w.th.joinable()) w.th.join();
+    }
+    workers_.clear();
+    for (Shard &s : shards_)
+      if (s.stream) {
+        int prev = -1;
+        (void)hipGetDevice(&prev);
+        (void)hipSetDevice(s.device);
+        (void)hipStreamSynchronize(s.stream);
+        (void)hipStreamDestroy(s.stream);
+        s.stream = nullptr;
+        if (prev >= 0) (void)hipSetDevice(prev);
+      }
+  }
+  // run f on every shard, each on its persistent worker thread; the first
+  // exception is rethrown
   template <class Fn>
   void each(Fn f) {
-    std::vector<std::exception_ptr> err(shards_.size());
-    std::vector<std::thread> th;
-    for (size_t g = 0; g < shards_.size(); ++g)
-      th.emplace_back([&, g] {
-        try {
-          f(shards_[g]);
-        } catch (...) {
-          err[g] = std::current_exception();
-        }
-      });
-    for (auto &t : th) t.join();
-    for (auto &e : err)
-      if (e) std::rethrow_exception(e);
+    if (workers_.empty()) {
+      for (Shard &sh : shards_) f(sh);
+      return;
+    }
+    std::lock_guard<std::mutex> turn(each_mu_);
+    for (size_t g = 0; g < shards_.size(); ++g) {
+      Worker &w = workers_[g];
+      {
+        std::lock_guard<std::mutex> lk(w.mu);
+        w.task = [&f, this, g] { f(shards_[g]); };
+        w.has = true;
+        w.done = false;
+        w.err = nullptr;
+      }
+      w.cv.notify_all();
+    }
+    std::exception_ptr first;
+    for (Worker &w : workers_) {
+      std::unique_lock<std::mutex> lk(w.mu);
+      w.cv.wait(lk, [&] { return w.done; });
+      if (w.err && !first) first = w.err;
+    }
+    if (first) std::rethrow_exception(first);
   }
   // split a reference-layout row range over the owning shards:
   // f(shard, first row within the shard, rows, offset into the caller's range)

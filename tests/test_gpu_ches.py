@@ -147,14 +147,14 @@ def test_mult_batch_matches_single(m, golden):
 @pytest.mark.parametrize("group,log_n,K", [(1, 16, 7), (2, 10, 7), (1, 12, 9), (1, 12, 17), (2, 10, 9),
                                            (2, 10, 17)])
 def test_mult_batch_sets_resident_and_pinned(m, group, log_n, K):
-    """Batches longer than every ring (Ches: front groups of kFrontGroup = 8 MSMs,
-    the first of one, in kFronts = 2 alternating front sets; kBSets = 2 bucket
+    """Batches longer than every ring (Ches: front groups ramping 1, 1, 2, 4, 8 MSMs,
+    in kFronts = 2 alternating front sets; kBSets = 2 bucket
     sets; host sets in 2 x 8 device slots copied on their own stream): K distinct
     sets from device memory and from page-locked host memory (streamed group by
     group inside the pipeline) equal the synchronous MSMs.  K = 9 and 17 also
     exceed one reduction group (kGroup = 8): several groups of uneven size R
     alternate between the two reducer buffer sets / tail streams and read back
-    at their own offsets, and the front groups (1 + 8 + 8) straddle them."""
+    at their own offsets, and the front groups (1, 1, 2, 4, 8, ...) straddle them."""
     import numpy as np
     import torch
     n = 1 << log_n
@@ -171,3 +171,45 @@ def test_mult_batch_sets_resident_and_pinned(m, group, log_n, K):
     assert [m.compress(group, r) for r in got_d] == want
     assert [m.compress(group, r) for r in got_h] == want
     ctx.close()
+
+
+_FRONT_GROUP_SCRIPT = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+import numpy as np, torch
+import msm_blst_amd as m
+ok = True
+for group, log_n, K in ((1, 12, 17), (2, 10, 9)):
+    n = 1 << log_n
+    ctx = m.CHESContext(group, 0, n_exp=log_n)
+    ctx.build_table(m.fixed_points(group, n), n)
+    host = torch.empty(K * n * 32, dtype=torch.uint8, pin_memory=True)
+    for k in range(K):
+        host.numpy()[k * n * 32:(k + 1) * n * 32] = np.frombuffer(m.gen_scalars(n, 300 + k), dtype=np.uint8)
+    dev = host.to("cuda:0")
+    torch.cuda.synchronize()
+    want = [m.compress(group, ctx.mult(dev.data_ptr() + k * n * 32, on_device=True)) for k in range(K)]
+    got_d = ctx.mult_batch(dev.data_ptr(), K, set_stride=n * 32, on_device=True)
+    got_h = ctx.mult_batch(host.data_ptr(), K, set_stride=n * 32, on_device=False)
+    ok &= [m.compress(group, r) for r in got_d] == want and [m.compress(group, r) for r in got_h] == want
+    ctx.close()
+print("FRONT_GROUPS_OK" if ok else "FRONT_GROUPS_MISMATCH")
+"""
+
+
+def test_batch_front_groups_of_eight():
+    """The grouped-front path (digits + sort of up to 8 MSMs in one pass per
+    stage; not the default, engine.hpp kFrontGroupDefault) selected with
+    MSM_FRONT_GROUP=8, which the library reads once per process: a child
+    process runs batches of 17 (G1) and 9 (G2) distinct sets -- front groups
+    1, 1, 2, 4, 8, 1 -- from device and pinned host memory against the
+    synchronous MSMs."""
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MSM_FRONT_GROUP="8")
+    r = subprocess.run([sys.executable, "-c", _FRONT_GROUP_SCRIPT, repo], capture_output=True, text=True, env=env,
+                       timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "FRONT_GROUPS_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]

@@ -113,5 +113,14 @@ def test_error_mode_returns_infinity_instead_of_abort(m):
         assert L.msm_error_pending() == 1
         assert L.msm_error_pending() == 0
         assert b"wbits" in L.msm_last_error()
+        # a failing precompute zeroes the caller's whole table (never half written)
+        wb = 15
+        tsz = L.blst_p1s_mult_wbits_precompute_sizeof(wb, n)
+        big = (ctypes.c_uint8 * tsz)(*([0xCD] * tsz))
+        P = (ctypes.c_uint8 * len(pts)).from_buffer_copy(pts)
+        pp = (ctypes.c_void_p * 2)(ctypes.cast(P, ctypes.c_void_p), None)
+        L.blst_p1s_mult_wbits_precompute(big, wb, pp, n)
+        assert L.msm_error_pending() == 1
+        assert bytes(big) == bytes(tsz)
     finally:
         L.msm_set_abort_on_error(prev)

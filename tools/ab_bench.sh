@@ -9,7 +9,7 @@ shift 2
 mkdir -p gpurun_out/$TAG
 for i in $(seq 1 $N); do
   for v in ${VARIANTS:-cur prev}; do
-    cp tools/ablib/libmsm_$v.so msm_blst_amd/libmsm_mi355x.so
+    cp tools/ablib/libmsm_$v.so msm_blst_amd/libmsm_mi355x.so || exit 1
     timeout -k 10 300 python -u bench.py --no-cpu-baseline "$@" > gpurun_out/$TAG/$v$i.json 2> gpurun_out/$TAG/$v$i.err || exit 1
   done
 done
