@@ -778,7 +778,10 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
   const size_t sslot = n * stride;  // one device scalar slot
   bool unsized = false;
   for (int f = 0; f < kFronts && (size_t)f < nfg; ++f) unsized |= fs_[f].sorted.bytes < n * (size_t)p_.h * fg_max * 4;
-  if (scalars_on_host || unsized) scal_.ensure(2 * fg_max * sslot + 16);
+  // host sets: nsg groups of fg_max device slots, copied up to nsg groups ahead
+  // (4 single-set groups -- as the round-2 pipeline's four slots -- or 2 larger)
+  const size_t nsg = fg_max == 1 ? 4 : 2;
+  if (scalars_on_host || unsized) scal_.ensure(std::max<size_t>(nsg, 2) * fg_max * sslot + 16);
   for (int f = 0; f < kFronts && (size_t)f < nfg; ++f)
     if (fs_[f].sorted.bytes < n * (size_t)p_.h * fg_max * 4) {
       MSM_HIP_CHECK(hipMemsetAsync(scal_.p, 0, fg_max * sslot, s));
@@ -788,17 +791,17 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
   const bool prof = profile_;
   profile_ = false;
   if (prof)
-    while (acc_ev_.size() < 2 * count) {
+    while (acc_ev_.size() < std::max<size_t>(2 * count, 2 * 64)) {
       hipEvent_t e;
       MSM_HIP_CHECK(hipEventCreate(&e));
       acc_ev_.push_back(e);
     }
   // Streams, front groups g (front set g % kFronts), bucket sets k % kBSets and,
-  // for host scalars, two groups of device scalar slots (g % 2):
+  // for host scalars, nsg groups of device scalar slots (g % nsg):
   //   fstream_:  digits + sort of front group g: ONE pass per stage over its R_g
-  //              scalar sets (bucket_sort.hpp), after group g - 2's accumulations
-  //              released the front set.  Issued when group g - 1's accumulations
-  //              are enqueued, so it runs beside them; at the greatest priority,
+  //              scalar sets (bucket_sort.hpp), after group g - 3's accumulations
+  //              released the front set.  Issued when group g - 2's accumulations
+  //              are enqueued, so it runs beside them or g - 1's; at the greatest priority,
   //              its short memory-bound kernels take the CU slots the
   //              accumulation's retiring workgroups free;
   //   s:         accumulation k into bucket set k % kBSets (after MSM k-2's
@@ -813,11 +816,12 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
   //              are paid once per group, not once per MSM.  Two streams: group
   //              q+1's level 0s never queue behind group q's tail;
   //   cstream_:  host scalars: the H2D copies of front group g's sets into slot
-  //              group g % 2, after front g - 2 consumed it, on their own stream.
+  //              group g % nsg, after front g - nsg consumed it, on their own stream.
   // No host waits inside the loop: every MSM has its own pinned read-back slot.
   // Reducer set t is reused by group q + 2 only after group q's tail: both are
   // in order on tails_[t].
-  while (bev_.size() < 3 * count + 2 * nfg + 1) {
+  // dependency events for at least 64 MSMs, created once (not inside a timed batch)
+  while (bev_.size() < std::max<size_t>(3 * count + 2 * nfg + 1, 3 * 64 + 2 * 64 + 1)) {
     hipEvent_t e;
     MSM_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     bev_.push_back(e);
@@ -827,10 +831,22 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
   MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, bev_[0], 0));
   MSM_HIP_CHECK(hipStreamWaitEvent(cstream_, bev_[0], 0));
   for (int t = 0; t < kBSets; ++t) MSM_HIP_CHECK(hipStreamWaitEvent(tails_[t], bev_[0], 0));
-  auto slots = [&](size_t g) { return scal_.as<uint8_t>() + (g % 2) * fg_max * sslot; };
+  auto slots = [&](size_t g) { return scal_.as<uint8_t>() + (g % nsg) * fg_max * sslot; };
+  // MSM_ZERO_COPY_SCALARS=1 (A/B knob): page-locked host sets are read by the
+  // digit kernel straight over PCIe instead of being copied by SDMA first
+  static const bool zc_env = [] {
+    const char *e = getenv("MSM_ZERO_COPY_SCALARS");
+    return e && atoi(e) != 0;
+  }();
+  bool zero_copy = false;
+  if (scalars_on_host && zc_env) {
+    hipPointerAttribute_t a;
+    zero_copy = hipPointerGetAttributes(&a, scalars) == hipSuccess && a.type == hipMemoryTypeHost;
+    if (!zero_copy) (void)hipGetLastError();
+  }
   auto copy_group = [&](size_t g) {
-    if (!scalars_on_host || g >= nfg) return;
-    if (g >= 2) MSM_HIP_CHECK(hipStreamWaitEvent(cstream_, evf[g - 2], 0));  // slots consumed by front g - 2
+    if (!scalars_on_host || zero_copy || g >= nfg) return;
+    if (g >= nsg) MSM_HIP_CHECK(hipStreamWaitEvent(cstream_, evf[g - nsg], 0));  // slots consumed by front g - nsg
     for (size_t k = fgb[g]; k < fgb[g + 1]; ++k)
       MSM_HIP_CHECK(hipMemcpyAsync(slots(g) + (k - fgb[g]) * sslot, scalars + k * set_stride, sslot,
                                    hipMemcpyHostToDevice, cstream_));
@@ -838,19 +854,20 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
   };
   auto front_group = [&](size_t g) {
     if (g >= nfg) return;
-    if (scalars_on_host) MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, evc[g], 0));
+    const bool copied = scalars_on_host && !zero_copy;
+    if (copied) MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, evc[g], 0));
     if (g >= (size_t)kFronts) MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, eva[fgb[g - kFronts + 1] - 1], 0));
-    const uint8_t *src = scalars_on_host ? slots(g) : scalars + fgb[g] * set_stride;
-    digits_sort(fstream_, src, stride, scalars_on_host ? sslot : set_stride, (int)(fgb[g + 1] - fgb[g]),
-                (int)(g % kFronts));
+    const uint8_t *src = copied ? slots(g) : scalars + fgb[g] * set_stride;
+    digits_sort(fstream_, src, stride, copied ? sslot : set_stride, (int)(fgb[g + 1] - fgb[g]), (int)(g % kFronts));
     MSM_HIP_CHECK(hipEventRecord(evf[g], fstream_));
   };
-  copy_group(0);
-  copy_group(1);
-  front_group(0);
+  for (size_t g = 0; g < nsg; ++g) copy_group(g);
+  // every group's copies are enqueued before its front (nsg >= kFronts - 1)
+  static_assert(kFronts - 1 <= 2, "copy lead must cover the front lead");
+  for (size_t g = 0; g + 1 < (size_t)kFronts; ++g) front_group(g);
   for (size_t g = 0; g < nfg; ++g) {
-    front_group(g + 1);  // beside this group's accumulations
-    copy_group(g + 2);
+    copy_group(g + nsg);
+    front_group(g + kFronts - 1);  // may start as soon as group g - 1's accumulations release its front set
     MSM_HIP_CHECK(hipStreamWaitEvent(s, evf[g], 0));
     for (size_t k = fgb[g]; k < fgb[g + 1]; ++k) {
       const int bset = (int)(k % kBSets), slot = (int)(k % R), gset = (int)((k / R) % 2);

@@ -320,8 +320,8 @@ class Ches {
   DevBuf code_, rank_, table_, buckets_[kBSets];
   // digit/sort outputs.  A batch can run the fronts (digits + sort) of up to
   // kFrontGroup MSMs in ONE pass per stage (seven launches for the group instead
-  // of seven per MSM), front group g+1 beside group g's accumulations, two front
-  // sets alternating.  Measured on MI355X (tools/ab_env.sh, profiles/
+  // of seven per MSM), front group g+2 beside group g's accumulations, three
+  // front sets in rotation.  Measured on MI355X (tools/ab_env.sh, profiles/
   // r03_front_group_ab.txt) the grouped fronts slow the accumulations they run
   // beside more than the launches they save (resident 2.33-2.38 ms per MSM with
   // groups of 8 vs 2.26-2.27 with groups of 1), so the default group is one
@@ -330,7 +330,7 @@ class Ches {
   static constexpr int kGroup = 8;       // batch: MSMs per reduction group (WeightedReducer::launch_tail_group)
   static constexpr int kFrontGroup = 8;  // batch: largest front group (ramping up 1, 1, 2, 4, 8)
   static constexpr int kFrontGroupDefault = 1;
-  static constexpr int kFronts = 2;
+  static constexpr int kFronts = 3;  // front k+1 may start when accumulation k-2 ends (slack for the copies)
   ChesFrontSet fs_[kFronts];
   // host scalar sets of a batch: two groups of kFrontGroup device slots, copied on
   // their own stream (cstream_) ahead of the group's front
