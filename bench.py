@@ -136,6 +136,9 @@ def main():
                     help="nccl = RCCL over xGMI (the multi-GPU bench); gloo only for --one-device rehearsals")
     ap.add_argument("--one-device", action="store_true",
                     help="rehearsal on a 1-GPU box: every rank uses device 0 (with --dist-backend gloo)")
+    ap.add_argument("--multi-context", type=int, default=0, metavar="D",
+                    help="N = 1: also time configs[3] (2^21 points) through ONE process driving D shards "
+                         "(msm_ches_ctx_create_multi; devices 0..D-1, or D shards on device 0 with --one-device)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -311,6 +314,12 @@ def main():
 
     if world == 1 and not args.no_compare and not args.no_configs and G == 1 and args.log_n == 20:
         others.update(config_legs(m, torch, dev, local, sp, pts, host, K, W))
+    # configs[3]: G1 n = 2^21 sharded over the ranks (RCCL path) or over the
+    # shards of one process (--multi-context), against the golden 2^21 result
+    if G == 1 and not args.no_compare and world > 1 and (1 << 21) % world == 0:
+        others.update(cfg3_ranks(m, mdist, torch, dev, local, sp, world, rank, K, W, xdev, add))
+    if G == 1 and world == 1 and args.multi_context > 1:
+        others.update(cfg3_multi_context(m, torch, args.multi_context, args.one_device, K, W))
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -573,6 +582,82 @@ def config_legs(m, torch, dev, local, sp, pts, host, K, W):
     c2.close()
     del d2
     return legs
+
+
+def _cfg3_sets(m, K, lo, hi):
+    """K scalar sets of the 2^21-point configs[3] problem, points [lo, hi) only:
+    set 0 = the seed-1 stream (golden), set k = seed 5000 + k; pinned host memory."""
+    import numpy as np
+    import torch
+    N = 1 << 21
+    n = hi - lo
+    host = torch.empty(K * n * 32, dtype=torch.uint8, pin_memory=True)
+    for k in range(K):
+        full = np.frombuffer(m.gen_scalars(N, 1 if k == 0 else 5000 + k), dtype=np.uint8)
+        host.numpy()[k * n * 32:(k + 1) * n * 32] = full[lo * 32:hi * 32]
+    return host
+
+
+def cfg3_ranks(m, mdist, torch, dev, local, sp, world, rank, K, W, xdev, add):
+    """configs[3] on the ranks: each rank builds the CHES table of its 2^21/world
+    points (ches_config_files for that shard size), multiplies its slices of K
+    distinct 2^21-scalar sets in one pipelined batch, then ONE all_gather (RCCL)
+    of the batch's partials and a host fold.  Strong scaling of a fixed 2^21."""
+    N = 1 << 21
+    lo, hi = mdist.shard_range(N, world, rank)
+    n = hi - lo
+    n_exp = n.bit_length() - 1
+    t = time.time()
+    ctx = m.CHESContext(1, local, n_exp=n_exp)
+    ctx.build_table(m.fixed_points(1, n, lo), n, stream=sp)
+    host = _cfg3_sets(m, K, lo, hi)
+    torch.cuda.synchronize(dev)
+    setup = time.time() - t
+    ctx.mult_batch(host.data_ptr(), min(max(W, 1), K), 32, set_stride=n * 32, on_device=False, stream=sp)
+    with Bracket(world, dev, xdev) as b:
+        parts = ctx.mult_batch(host.data_ptr(), K, 32, set_stride=n * 32, on_device=False, stream=sp)
+        res = [mdist.fold(ps, add) for ps in mdist.gather_partials_batch(parts, 1, xdev)]
+    want = _golden(m, 1, N)
+    ok = all_true(m.compress(1, res[0]).hex() == want, world, xdev)
+    ctx.close()
+    return {"cfg3_2^21_ranks": {
+        "value": round(N * K / b.elapsed, 1), "unit": "pairs/s", "ms_per_step": round(b.elapsed / K * 1e3, 4),
+        "parity_vs_reference": ok, "setup_s": round(setup, 2), "points_per_rank": n,
+        "note": f"configs[3]: G1 n=2^21 over {world} ranks ({n} points each, config_file_n_exp_{n_exp}.h), "
+                f"{K} distinct scalar sets H2D from pinned memory, one RCCL all_gather of the batch's partials"}}
+
+
+def cfg3_multi_context(m, torch, D, one_device, K, W):
+    """configs[3] through ONE process driving D shards (msm_ches_ctx_create_multi:
+    persistent shard workers, host fold)."""
+    N = 1 << 21
+    n = N // D
+    n_exp = n.bit_length() - 1
+    devs = [0] * D if one_device else list(range(D))
+    t = time.time()
+    ctx = m.CHESContext(1, n_exp=n_exp, devices=devs)
+    ctx.build_table(m.fixed_points(1, N), N)
+    host = _cfg3_sets(m, K, 0, N)
+    setup = time.time() - t
+    ctx.mult(host.data_ptr())
+    ctx.mult_batch(host.data_ptr(), min(max(W, 1), K), 32, set_stride=N * 32)
+    for d in set(devs):
+        torch.cuda.synchronize(d)
+    t = time.perf_counter()
+    res = ctx.mult_batch(host.data_ptr(), K, 32, set_stride=N * 32)
+    el = time.perf_counter() - t
+    t = time.perf_counter()
+    sres = [ctx.mult(host.data_ptr() + k * N * 32) for k in range(min(K, 5))]
+    sel = (time.perf_counter() - t) / min(K, 5)
+    want = _golden(m, 1, N)
+    eq = [m.compress(1, x) for x in sres] == [m.compress(1, x) for x in res[:len(sres)]]
+    ctx.close()
+    return {"cfg3_2^21_multi_context": {
+        "value": round(N * K / el, 1), "unit": "pairs/s", "ms_per_step": round(el / K * 1e3, 4),
+        "sync_ms_per_msm": round(sel * 1e3, 4), "parity_vs_reference": m.compress(1, res[0]).hex() == want,
+        "batch_equals_sync": eq, "setup_s": round(setup, 2), "devices": devs,
+        "note": f"configs[3] in ONE process: {D} shards of {n} points (config_file_n_exp_{n_exp}.h) on devices "
+                f"{sorted(set(devs))}, msm_ches_ctx_create_multi, {K} distinct sets from pinned host memory"}}
 
 
 def _ref_lib(name):
