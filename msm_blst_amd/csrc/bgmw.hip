@@ -171,7 +171,7 @@ void Bgmw<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, hfp::J
   const size_t n = n_, ne = n * (size_t)h_, NB = bucket_count();
   keys_.ensure(ne * 4);
   vals_.ensure(ne * 4);
-  sorted_.ensure(ne * 4);
+  sorted_.ensure(ne * 4 + 64);  // + the accumulation's 16-B payload window past a run's end
   counts_.ensure(NB * 4);
   offsets_.ensure(NB * 4);
   order_.ensure(NB * 4);
@@ -184,7 +184,7 @@ void Bgmw<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, hfp::J
   sort_.run(s, keys_.as<uint32_t>(), vals_.as<uint32_t>(), ne, (uint32_t)NB, sorted_.as<uint32_t>(),
             counts_.as<uint32_t>(), offsets_.as<uint32_t>(), order_.as<uint32_t>());
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[2], s));
-  launch_accumulate<G>(s, order_.as<uint32_t>(), counts_.as<uint32_t>(), offsets_.as<uint32_t>(),
+  launch_accumulate<G>(s, order_.as<uint32_t>(), sort_.sched_counts(), sort_.sched_offsets(),
                        sorted_.as<uint32_t>(), table_.as<AffP<F>>(), buckets_.as<Xyzz<F>>(), NB);
   MSM_HIP_CHECK(hipGetLastError());
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[3], s));

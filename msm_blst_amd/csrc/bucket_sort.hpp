@@ -329,14 +329,21 @@ static __global__ void __launch_bounds__(1024)
 // ids.  The order inside a class is arbitrary.  A block covers 4096 buckets so
 // that the ~20 busy class cursors see a few hundred atomics, not one per 256
 // buckets (a single address saturates at ~88 atomics/us, MI355X_MICROARCH.md).
+// The bucket's count and payload offset are written beside its id in schedule
+// order (scnt / soff), so the accumulation reads them coalesced by lane instead
+// of two random 4-B loads (two 64-B lines) per bucket.
 static __global__ void __launch_bounds__(256)
-    k_sched_scatter(const uint32_t *__restrict__ counts, uint32_t nb, uint32_t *__restrict__ class_total,
-                    uint32_t *__restrict__ order) {
+    k_sched_scatter(const uint32_t *__restrict__ counts, const uint32_t *__restrict__ offsets, uint32_t nb,
+                    uint32_t *__restrict__ class_total, uint32_t *__restrict__ order, uint32_t *__restrict__ scnt,
+                    uint32_t *__restrict__ soff) {
   __shared__ uint32_t h[256];
   __shared__ uint32_t base[256];
   __shared__ uint32_t wsum[4];
   counts += (size_t)blockIdx.y * nb;
+  offsets += (size_t)blockIdx.y * nb;
   order += (size_t)blockIdx.y * nb;
+  scnt += (size_t)blockIdx.y * nb;
+  soff += (size_t)blockIdx.y * nb;
   class_total += (size_t)blockIdx.y * 512;
   const uint32_t t = threadIdx.x, b0 = blockIdx.x * SCHED_PER_BLOCK, lane = t & 63, wave = t >> 6;
   h[t] = 0;
@@ -352,11 +359,12 @@ static __global__ void __launch_bounds__(256)
   __syncthreads();
   uint32_t cbase = incl - v;
   for (uint32_t w = 0; w < wave; ++w) cbase += wsum[w];
-  uint32_t cls[SCHED_PER_THREAD], rank[SCHED_PER_THREAD];
+  uint32_t cls[SCHED_PER_THREAD], rank[SCHED_PER_THREAD], cnt[SCHED_PER_THREAD];
 #pragma unroll
   for (int r = 0; r < SCHED_PER_THREAD; ++r) {
     const uint32_t b = b0 + r * 256 + t;
-    cls[r] = b < nb ? sched_class(counts[b]) : 0u;
+    cnt[r] = b < nb ? counts[b] : 0u;
+    cls[r] = sched_class(cnt[r]);
     rank[r] = b < nb ? atomicAdd(&h[cls[r]], 1u) : 0u;
   }
   __syncthreads();
@@ -365,7 +373,12 @@ static __global__ void __launch_bounds__(256)
 #pragma unroll
   for (int r = 0; r < SCHED_PER_THREAD; ++r) {
     const uint32_t b = b0 + r * 256 + t;
-    if (b < nb) order[base[cls[r]] + rank[r]] = b;
+    if (b < nb) {
+      const uint32_t pos = base[cls[r]] + rank[r];
+      order[pos] = b;
+      scnt[pos] = cnt[r];
+      soff[pos] = offsets[b];
+    }
   }
 }
 

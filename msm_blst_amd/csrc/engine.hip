@@ -52,8 +52,10 @@ void BucketSort::run(hipStream_t s, const uint32_t *keys, const uint32_t *vals, 
                      fb_bits, ncb, ntiles, gbase.as<uint32_t>(), ghist.as<uint32_t>(), nb, sorted, counts, offsets,
                      classes.as<uint32_t>(), nsets);
   MSM_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(k_sched_scatter, dim3(nblk(nb, SCHED_PER_BLOCK), nsets), dim3(256), 0, s, counts, nb,
-                     classes.as<uint32_t>(), order);
+  scnt.ensure((size_t)nb * nsets * 4);
+  soff.ensure((size_t)nb * nsets * 4);
+  hipLaunchKernelGGL(k_sched_scatter, dim3(nblk(nb, SCHED_PER_BLOCK), nsets), dim3(256), 0, s, counts, offsets, nb,
+                     classes.as<uint32_t>(), order, scnt.as<uint32_t>(), soff.as<uint32_t>());
   MSM_HIP_CHECK(hipGetLastError());
 }
 #endif
@@ -129,7 +131,7 @@ void Pippenger<G>::front(hipStream_t s, const uint8_t *d_scalars, size_t stride,
   const size_t n = n_, ne = (size_t)W * n;
   keys_.ensure(ne * 4);
   vals_.ensure(ne * 4);
-  sorted_.ensure(ne * 4);
+  sorted_.ensure(ne * 4 + 64);  // + the accumulation's 16-B payload window past a run's end
   counts_.ensure(NT * 4);
   offsets_.ensure(NT * 4);
   order_.ensure(NT * 4);
@@ -151,7 +153,7 @@ void Pippenger<G>::back(hipStream_t s, int nbits, hfp::Jac<HF> *out) {
   const size_t NB = (size_t)1 << (c - 1);
   const size_t NT = (size_t)W * NB;
   buckets_.ensure(NT * sizeof(Xyzz<F>));
-  launch_accumulate<G>(s, order_.as<uint32_t>(), counts_.as<uint32_t>(), offsets_.as<uint32_t>(),
+  launch_accumulate<G>(s, order_.as<uint32_t>(), sort_.sched_counts(), sort_.sched_offsets(),
                        sorted_.as<uint32_t>(), pts_.as<Aff<F>>(), buckets_.as<Xyzz<F>>(), NT);
   MSM_HIP_CHECK(hipGetLastError());
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[3], s));

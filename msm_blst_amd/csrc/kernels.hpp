@@ -256,9 +256,34 @@ static __global__ void k_iota(uint32_t *a, size_t n) {
 #ifndef MSM_ACC_WAVES
 #define MSM_ACC_WAVES 3
 #endif
+// Payload entries of one bucket's run, read 16 B at a time: the lanes of a
+// wave walk 64 different runs, so a 4-B load per step fetches 64 distinct
+// lines that are evicted (by the point loads) before the next step; an aligned
+// 4-entry window fetches each line once per 4 steps.  The payload buffer is
+// allocated with 64 B of slack, so a window past the last run's end stays in
+// bounds.
+struct PayloadWindow {
+  const uint4 *base;
+  uint4 w;
+  uint32_t pos;
+  MSM_FN PayloadWindow(const uint32_t *sorted, uint32_t off, uint32_t cnt)
+      : base(reinterpret_cast<const uint4 *>(sorted)), pos(off) {
+    if (cnt) w = base[off >> 2];
+  }
+  MSM_FN uint32_t next() {
+    const uint32_t q = pos & 3;
+    const uint32_t e = q == 0 ? w.x : q == 1 ? w.y : q == 2 ? w.z : w.w;
+    ++pos;
+    if ((pos & 3) == 0) w = base[pos >> 2];  // may read the slack after the run: unused
+    return e;
+  }
+};
+
 // One lane per bucket, buckets visited in the schedule `order` (descending
 // entry count, BucketSort) so the 64 lanes of a wave run loops of nearly equal
-// length and the longest buckets start first.
+// length and the longest buckets start first.  counts / offsets are indexed by
+// schedule position (BucketSort scnt / soff: coalesced); `order` gives the
+// bucket the sum is stored to.
 template <int G, class PT = Aff<typename FieldOf<G>::F>>
 __global__ void __launch_bounds__(256, MSM_ACC_WAVES) k_accumulate(const uint32_t *__restrict__ order,
                                                     const uint32_t *__restrict__ counts,
@@ -269,17 +294,17 @@ __global__ void __launch_bounds__(256, MSM_ACC_WAVES) k_accumulate(const uint32_
   typedef typename FieldOf<G>::F F;
   size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= nbuckets) return;
-  uint32_t id = order[t];
-  uint32_t cnt = counts[id], off = offsets[id];
+  const uint32_t cnt = counts[t];
+  PayloadWindow pw(sorted, offsets[t], cnt);
   Xyzz<F> acc;
   xyzz_set_inf(acc);
   for (uint32_t k = 0; k < cnt; ++k) {
-    uint32_t e = sorted[off + k];
+    const uint32_t e = pw.next();
     Aff<F> p = ld_point(&pts[e & 0x7fffffffu]);
     if (f_is_zero_exact(p.x) && f_is_zero_exact(p.y)) continue;  // affine infinity (ec_ops.h:717)
     xyzz_madd(acc, p, (e >> 31) != 0);
   }
-  st16(&buckets[id], acc);
+  st16(&buckets[order[t]], acc);
 }
 
 // One level of the bucket reduction.  Invariant per window:

@@ -53,18 +53,18 @@ __global__ void __launch_bounds__(256) k_accumulate2p(const uint32_t *__restrict
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= 2 * nbuckets) return;  // whole pairs only: 2 nbuckets lanes
   const int comp = (int)(t & 1);
-  const uint32_t id = order[t >> 1];
-  const uint32_t cnt = counts[id], off = offsets[id];
+  const uint32_t cnt = counts[t >> 1];  // schedule-ordered (k_accumulate)
+  PayloadWindow pw(sorted, offsets[t >> 1], cnt);
   Xyzz<Fp2L> acc;
   xyzz_set_inf(acc);
   for (uint32_t k = 0; k < cnt; ++k) {
-    const uint32_t e = sorted[off + k];
+    const uint32_t e = pw.next();
     Aff<Fp2L> p;
     ld_point2l(p, &pts[e & 0x7fffffffu], comp);
     if (f_is_zero_exact(p.x) && f_is_zero_exact(p.y)) continue;  // affine infinity (ec_ops.h:717)
     xyzz_madd(acc, p, (e >> 31) != 0);
   }
-  st_xyzz2l(&buckets[id], acc, comp);
+  st_xyzz2l(&buckets[order[t >> 1]], acc, comp);
 }
 
 // k_segsum (ches_kernels.hpp) for G2 with two lanes per output
