@@ -184,8 +184,8 @@ void Bgmw<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, hfp::J
   sort_.run(s, keys_.as<uint32_t>(), vals_.as<uint32_t>(), ne, (uint32_t)NB, sorted_.as<uint32_t>(),
             counts_.as<uint32_t>(), offsets_.as<uint32_t>(), order_.as<uint32_t>());
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[2], s));
-  launch_accumulate<G>(s, order_.as<uint32_t>(), sort_.sched_counts(), sort_.sched_offsets(),
-                       sorted_.as<uint32_t>(), table_.as<AffP<F>>(), buckets_.as<Xyzz<F>>(), NB);
+  launch_accumulate<G>(s, sort_.sched(order_.as<uint32_t>(), sorted_.as<uint32_t>(), 0, NB), table_.as<AffP<F>>(),
+                       buckets_.as<Xyzz<F>>(), NB);
   MSM_HIP_CHECK(hipGetLastError());
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[3], s));
   red_.launch(s, buckets_.p);

@@ -382,5 +382,83 @@ static __global__ void __launch_bounds__(256)
   }
 }
 
+// Interleaved payload.  The 64 lanes of an accumulation wave walk 64 buckets
+// of nearly equal count (the schedule above); with the payload in bucket order
+// step k of the wave reads 64 scattered 4-B entries -- 64 line fetches, the
+// lines evicted (by the point loads) before step k + 1.  Wave group w of 64
+// schedule positions instead gets a block of head(w) rows of 64 entries, head
+// = the count at its first position (the largest: the schedule is sorted by
+// exact count below 255); row k holds entry k of each of its buckets, so step
+// k is one coalesced 256-B read.  Groups that start inside class 0 (counts >=
+// 255, not sorted) keep the bucket-ordered payload (wbase = ~0).  The blocks
+// need no scan: the count at a position follows from the class totals, so
+// group w's first row is sum over the earlier interleaved groups of their
+// heads, computed per class from the totals in LDS.  Size: head(w) <= the
+// smallest count of group w - 1, so the rows of all groups but the first fit
+// in the entries of their predecessors: <= ne + 64 * 255 per set.
+constexpr size_t BS_IPAY_SLACK = 64 * 256;
+static __global__ void __launch_bounds__(256)
+    k_interleave(const uint32_t *__restrict__ scnt, const uint32_t *__restrict__ soff, uint32_t nb, uint32_t nw,
+                 const uint32_t *__restrict__ class_total, const uint32_t *__restrict__ sorted,
+                 uint32_t *__restrict__ ipay, size_t ipay_stride, uint32_t *__restrict__ wbase) {
+  __shared__ uint32_t ct[256], hs[256], wsum[4];
+  const size_t set = blockIdx.y;
+  const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const uint32_t tot = class_total[set * 512 + t];
+  // exclusive scan of the class totals (class order = position order)
+  uint32_t incl = tot;
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t u = __shfl_up(incl, d, 64);
+    if (lane >= (uint32_t)d) incl += u;
+  }
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  uint32_t c0 = incl - tot;
+  for (uint32_t w = 0; w < wave; ++w) c0 += wsum[w];
+  ct[t] = c0;
+  __syncthreads();
+  const uint32_t t0r = (ct[1] + 63) & ~63u;  // first interleaved position (class 0 = ct[0] .. ct[1])
+  // heads of class t: multiples of 64 in [max(ct, t0r), ct + tot), each a row block of 255 - t rows
+  const uint32_t lo = max(c0, t0r), hi = c0 + tot;
+  const uint32_t contrib = (t > 0 && lo < hi) ? (255u - t) * (((hi + 63) >> 6) - ((lo + 63) >> 6)) : 0u;
+  __syncthreads();
+  incl = contrib;
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t u = __shfl_up(incl, d, 64);
+    if (lane >= (uint32_t)d) incl += u;
+  }
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  uint32_t h0 = incl - contrib;
+  for (uint32_t w = 0; w < wave; ++w) h0 += wsum[w];
+  hs[t] = h0;
+  __syncthreads();
+  const uint32_t p = blockIdx.x * 256 + t;
+  const uint32_t g = p >> 6, head = g << 6;
+  uint32_t base = ~0u;
+  if (head >= t0r && head < nb) {
+    // class of the head position: the last c with ct[c] <= head (empty classes
+    // share ct with their successor, so the last such c is non-empty)
+    uint32_t c = 0;
+    for (uint32_t step = 128; step; step >>= 1)
+      if (ct[c + step] <= head) c += step;
+    const uint32_t first = max(ct[c], t0r);
+    base = hs[c] + (255u - c) * ((head >> 6) - ((first + 63) >> 6));
+  }
+  if (lane == 0 && g < nw) wbase[set * nw + g] = base;
+  if (base == ~0u || p >= nb) return;
+  const uint32_t n = scnt[set * nb + p], o = soff[set * nb + p];
+  uint32_t *dst = ipay + set * ipay_stride + (size_t)base * 64 + lane;
+  const uint32_t *src = sorted + o;
+  uint32_t k = 0;
+  for (; k + 4 <= n; k += 4) {  // four loads in flight per lane
+    const uint32_t a = src[k], b = src[k + 1], c = src[k + 2], d = src[k + 3];
+    dst[(size_t)k * 64] = a;
+    dst[(size_t)(k + 1) * 64] = b;
+    dst[(size_t)(k + 2) * 64] = c;
+    dst[(size_t)(k + 3) * 64] = d;
+  }
+  for (; k < n; ++k) dst[(size_t)k * 64] = src[k];
+}
 
 }  // namespace msm

@@ -641,7 +641,7 @@ void Ches<G>::digits_sort(hipStream_t s, const uint8_t *d_scalars, size_t stride
   ChesFrontSet &f = fs_[set];
   f.keys.ensure(ne * nsets * 4);
   f.vals.ensure(ne * nsets * 4);
-  f.sorted.ensure(ne * nsets * 4);
+  f.sorted.ensure(ne * nsets * 4 + 64);  // + the accumulation's 16-B payload window past a run's end
   f.counts.ensure(NB * nsets * 4);
   f.offsets.ensure(NB * nsets * 4);
   f.order.ensure(NB * nsets * 4);
@@ -671,8 +671,7 @@ void Ches<G>::accumulate(hipStream_t s, int set, int r, int bset) {
   const size_t NB = bucket_count();
   ChesFrontSet &f = fs_[set];
   buckets_[bset].ensure(NB * sizeof(Xyzz<F>));
-  launch_accumulate<G>(s, f.order.as<uint32_t>() + r * NB, f.counts.as<uint32_t>() + r * NB,
-                       f.offsets.as<uint32_t>() + r * NB, f.sorted.as<uint32_t>(), table_.as<AffP<F>>(),
+  launch_accumulate<G>(s, f.sort.sched(f.order.as<uint32_t>(), f.sorted.as<uint32_t>(), r, NB), table_.as<AffP<F>>(),
                        buckets_[bset].as<Xyzz<F>>(), NB);
   MSM_HIP_CHECK(hipGetLastError());
 }
@@ -736,6 +735,11 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
       MSM_HIP_CHECK(hipEventCreateWithFlags(&ev_tail_[t], hipEventDisableTiming));
     }
     MSM_HIP_CHECK(hipStreamCreateWithFlags(&cstream_, hipStreamNonBlocking));
+    // a stream's hardware queue is set up at its first launch: do that here,
+    // not inside the first batch that happens to use the stream
+    prime_.ensure(256);
+    for (hipStream_t q : {fstream_, tails_[0], tails_[1], cstream_}) MSM_HIP_CHECK(hipMemsetAsync(prime_.p, 0, 256, q));
+    for (hipStream_t q : {fstream_, tails_[0], tails_[1], cstream_}) MSM_HIP_CHECK(hipStreamSynchronize(q));
   }
   // one pinned read-back slot per MSM of the batch: the host never waits inside
   // the issue loop, so MSM k+1's front is queued while MSM k still accumulates
@@ -768,21 +772,23 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
   // every buffer the loop touches exists before the first launch (an allocation
   // inside the issue loop could synchronise the device)
   const size_t NB = bucket_count(), n = n_;
-  for (int b = 0; b < kBSets && (size_t)b < count; ++b) buckets_[b].ensure(NB * sizeof(Xyzz<typename FieldOf<G>::F>));
+  for (int b = 0; b < kBSets; ++b) buckets_[b].ensure(NB * sizeof(Xyzz<typename FieldOf<G>::F>));
   // sized for kGroup whatever this batch's R: a later, larger batch must not
   // reallocate (a hipFree inside the pipelined region would synchronise it)
-  for (int t = 0; t < kBSets && (size_t)t < ngroups; ++t) red_.ensure_group(t, kGroup);
+  // (both reducer sets, and both bucket sets, whatever this batch's length: a
+  // short warm-up batch must leave nothing to allocate inside a longer one)
+  for (int t = 0; t < kBSets; ++t) red_.ensure_group(t, kGroup);
   // front sets sized for a whole front group (the sort's scan scratch too): run
   // one sort of fg_max sets per set before the loop if they are not yet sized
   // (fg_max dummy sets of all-zero scalars, outside the batch timing)
   const size_t sslot = n * stride;  // one device scalar slot
   bool unsized = false;
-  for (int f = 0; f < kFronts && (size_t)f < nfg; ++f) unsized |= fs_[f].sorted.bytes < n * (size_t)p_.h * fg_max * 4;
+  for (int f = 0; f < kFronts; ++f) unsized |= fs_[f].sorted.bytes < n * (size_t)p_.h * fg_max * 4;
   // host sets: nsg groups of fg_max device slots, copied up to nsg groups ahead
   // (4 single-set groups -- as the round-2 pipeline's four slots -- or 2 larger)
   const size_t nsg = fg_max == 1 ? 4 : 2;
   if (scalars_on_host || unsized) scal_.ensure(std::max<size_t>(nsg, 2) * fg_max * sslot + 16);
-  for (int f = 0; f < kFronts && (size_t)f < nfg; ++f)
+  for (int f = 0; f < kFronts; ++f)
     if (fs_[f].sorted.bytes < n * (size_t)p_.h * fg_max * 4) {
       MSM_HIP_CHECK(hipMemsetAsync(scal_.p, 0, fg_max * sslot, s));
       digits_sort(s, scal_.as<uint8_t>(), stride, sslot, (int)fg_max, f);

@@ -376,6 +376,11 @@ static __global__ void __launch_bounds__(256)
 }
 
 // ------------------------------------------------------------ segment sums --
+// MSM_SEGSUM_PREFETCH=1 (A/B build knob): load the next operand before the
+// current add (G1: 149 -> 218 VGPRs, 3 -> 2 waves per SIMD)
+#ifndef MSM_SEGSUM_PREFETCH
+#define MSM_SEGSUM_PREFETCH 0
+#endif
 // dst[t] = sum_{k in [starts[t], starts[t+1])} src[idx ? idx[k] : k]   (xyzz)
 // for each of gridDim.y MSMs of a batch group: MSM blockIdx.y reads src +
 // y src_stride and writes dst + y dst_stride (the same plan for every MSM)
@@ -395,10 +400,22 @@ static __global__ void __launch_bounds__(256)
     xyzz_set_inf(acc);
   } else {
     acc = ld16(&src[idx ? idx[lo] : lo]);
+    // the next operand is loaded before the current add: its (random, L2-missing)
+    // load overlaps ~3.5 k instructions of the add instead of stalling the lane
+#if MSM_SEGSUM_PREFETCH
+    Xyzz<F> nxt;
+    if (lo + 1 < hi) nxt = ld16(&src[idx ? idx[lo + 1] : lo + 1]);
+    for (uint32_t k = lo + 1; k < hi; ++k) {
+      Xyzz<F> a = nxt;
+      if (k + 1 < hi) nxt = ld16(&src[idx ? idx[k + 1] : k + 1]);
+      xyzz_add(acc, a);
+    }
+#else
     for (uint32_t k = lo + 1; k < hi; ++k) {
       Xyzz<F> a = ld16(&src[idx ? idx[k] : k]);
       xyzz_add(acc, a);
     }
+#endif
   }
   st16(&dst[t], acc);
 }

@@ -89,8 +89,8 @@ void entry_msm(void *ret, const void *pts_blst, size_t npts, const uint32_t *key
   S.buckets.ensure(nb * sizeof(Xyzz<F>));
   S.sort.run(s, S.keys.template as<uint32_t>(), S.vals.template as<uint32_t>(), ne, (uint32_t)nb, S.sorted.template as<uint32_t>(),
              S.counts.template as<uint32_t>(), S.offsets.template as<uint32_t>(), S.order.template as<uint32_t>());
-  launch_accumulate<G>(s, S.order.template as<uint32_t>(), S.sort.sched_counts(), S.sort.sched_offsets(),
-                       S.sorted.template as<uint32_t>(), S.pts.template as<Aff<F>>(),
+  launch_accumulate<G>(s, S.sort.sched(S.order.template as<uint32_t>(), S.sorted.template as<uint32_t>(), 0, nb),
+                       S.pts.template as<Aff<F>>(),
                        S.buckets.template as<Xyzz<F>>(), nb);
   MSM_HIP_CHECK(hipGetLastError());
   if (buckets_out) {

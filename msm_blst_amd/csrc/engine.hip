@@ -36,6 +36,10 @@ void BucketSort::run(hipStream_t s, const uint32_t *keys, const uint32_t *vals, 
   gbase.ensure(nslots * 4);
   okeys.ensure(std::max<size_t>(ne * nsets, 1) * 4);
   ovals.ensure(std::max<size_t>(ne * nsets, 1) * 4);
+  const size_t nw = groups(nb);
+  wbase.ensure(nw * nsets * 4);
+  ipay_stride = ne + BS_IPAY_SLACK;
+  ipay.ensure(ipay_stride * nsets * 4);
   size_t scan_tmp = 0;
   hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, ghist.as<uint32_t>(), gbase.as<uint32_t>(), (int)nslots, s);
   tmp.ensure(scan_tmp);
@@ -56,6 +60,10 @@ void BucketSort::run(hipStream_t s, const uint32_t *keys, const uint32_t *vals, 
   soff.ensure((size_t)nb * nsets * 4);
   hipLaunchKernelGGL(k_sched_scatter, dim3(nblk(nb, SCHED_PER_BLOCK), nsets), dim3(256), 0, s, counts, offsets, nb,
                      classes.as<uint32_t>(), order, scnt.as<uint32_t>(), soff.as<uint32_t>());
+  MSM_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(k_interleave, dim3((unsigned)nw / 4 + 1, nsets), dim3(256), 0, s, scnt.as<uint32_t>(),
+                     soff.as<uint32_t>(), nb, (uint32_t)nw, classes.as<uint32_t>(), sorted, ipay.as<uint32_t>(),
+                     ipay_stride, wbase.as<uint32_t>());
   MSM_HIP_CHECK(hipGetLastError());
 }
 #endif
@@ -153,8 +161,8 @@ void Pippenger<G>::back(hipStream_t s, int nbits, hfp::Jac<HF> *out) {
   const size_t NB = (size_t)1 << (c - 1);
   const size_t NT = (size_t)W * NB;
   buckets_.ensure(NT * sizeof(Xyzz<F>));
-  launch_accumulate<G>(s, order_.as<uint32_t>(), sort_.sched_counts(), sort_.sched_offsets(),
-                       sorted_.as<uint32_t>(), pts_.as<Aff<F>>(), buckets_.as<Xyzz<F>>(), NT);
+  launch_accumulate<G>(s, sort_.sched(order_.as<uint32_t>(), sorted_.as<uint32_t>(), 0, NT), pts_.as<Aff<F>>(),
+                       buckets_.as<Xyzz<F>>(), NT);
   MSM_HIP_CHECK(hipGetLastError());
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[3], s));
   const int tcl = top_copies_log2(nbits);

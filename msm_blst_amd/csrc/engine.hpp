@@ -9,6 +9,7 @@
 #include <string>
 #include <vector>
 
+#include "acc_sched.hpp"
 #include "host_fp.hpp"
 
 #define MSM_HIP_CHECK(x)                                                                           \
@@ -71,13 +72,32 @@ struct HostField<2> {
 // accumulation schedule (bucket ids by descending count).
 struct BucketSort {
   DevBuf ghist, gbase, okeys, ovals, classes, tmp;
+  // the schedule's per-position count and payload offset (scnt[t] = counts[order[t]],
+  // soff[t] = offsets[order[t]]), the wave groups' interleaved rows (wlen, wbase)
+  // and the interleaved payload
+  DevBuf scnt, soff, wbase, ipay;
+  size_t ipay_stride = 0;  // interleaved entries per set (ne + BS_IPAY_SLACK)
+  static size_t groups(size_t nb) { return (nb + 63) / 64; }
+  // set `set` of the last run (nb buckets per set); order/sorted as passed to run
+  AccSched sched(const uint32_t *order, const uint32_t *sorted, size_t set, size_t nb) const {
+    const size_t nw = groups(nb);
+    return AccSched{order + set * nb,
+                    scnt.as<uint32_t>() + set * nb,
+                    soff.as<uint32_t>() + set * nb,
+                    wbase.as<uint32_t>() + set * nw,
+                    ipay.as<uint32_t>() + set * ipay_stride,
+                    sorted};
+  }
   // keys[ne] (bucket < nb or 0xffffffff), vals[ne]; outputs sized ne / nb.
   // nsets > 1: nsets independent sorts in the same launches -- inputs at
   // keys/vals + r ne, outputs counts/offsets/order + r nb (offsets index the one
   // shared `sorted` array of up to nsets ne entries), bucket_sort.hpp
   void run(hipStream_t s, const uint32_t *keys, const uint32_t *vals, size_t ne, uint32_t nb, uint32_t *sorted,
            uint32_t *counts, uint32_t *offsets, uint32_t *order, int nsets = 1);
-  size_t device_bytes() const { return ghist.bytes + gbase.bytes + okeys.bytes + ovals.bytes + classes.bytes + tmp.bytes; }
+  size_t device_bytes() const {
+    return ghist.bytes + gbase.bytes + okeys.bytes + ovals.bytes + classes.bytes + tmp.bytes + scnt.bytes + soff.bytes +
+           wbase.bytes + ipay.bytes;
+  }
 };
 
 // Dense windowed bucket reduction: for each of W windows of S buckets
@@ -335,6 +355,7 @@ class Ches {
   // host scalar sets of a batch: two groups of kFrontGroup device slots, copied on
   // their own stream (cstream_) ahead of the group's front
   DevBuf scal_;
+  DevBuf prime_;  // target of the one-time stream priming launches (run_batch)
   WeightedReducer<G> red_;
   std::vector<hipEvent_t> ev_;
   hipStream_t tails_[kBSets] = {nullptr, nullptr}, fstream_ = nullptr, cstream_ = nullptr;  // batch streams (+ the caller's)

@@ -35,9 +35,9 @@
 #define MSM_FN inline
 #define MSM_CONST constexpr
 extern "C" int msm_fp_overflow;
-#define MSM_CHECK(c)                 \
-  do {                               \
-    if (!(c)) msm_fp_overflow = 1;   \
+#define MSM_CHECK(c)                                                    \
+  do {                                                                  \
+    if (!(c)) __atomic_store_n(&msm_fp_overflow, 1, __ATOMIC_RELAXED);  \
   } while (0)
 #else
 #include <hip/hip_runtime.h>

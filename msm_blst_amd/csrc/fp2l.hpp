@@ -23,9 +23,18 @@ struct Fp2L {
   Fp c;  // this lane's component: c0 on even lanes, c1 on odd lanes
 };
 
+#ifdef MSM_FP_HOST_TEST
+// host range-check build (tests/host/fp_host_shim.cpp): the pair is two host
+// threads run in lockstep, and the partner's value comes through the shim
+extern "C" int msm_host_lane(void);
+extern "C" uint32_t msm_host_pair_swap(uint32_t x);
+MSM_FN bool pair_odd() { return (msm_host_lane() & 1) != 0; }
+MSM_FN uint32_t pair_swap(uint32_t x) { return msm_host_pair_swap(x); }
+#else
 MSM_FN bool pair_odd() { return (__lane_id() & 1) != 0; }
 // the partner lane's value (DPP quad_perm [1,0,3,2]: lanes 2k <-> 2k+1)
 MSM_FN uint32_t pair_swap(uint32_t x) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, true); }
+#endif
 MSM_FN void pair_swap(Fp &r, const Fp &a) {
 #pragma unroll
   for (int i = 0; i < NL; ++i) r.v[i] = pair_swap(a.v[i]);

@@ -13,6 +13,7 @@
 //   k_finalize    window totals -> blst Jacobian (R=2^384 Montgomery)
 // CHES pipeline: see ches.hpp.
 #pragma once
+#include "acc_sched.hpp"
 #include "ec.hpp"
 
 namespace msm {
@@ -256,55 +257,47 @@ static __global__ void k_iota(uint32_t *a, size_t n) {
 #ifndef MSM_ACC_WAVES
 #define MSM_ACC_WAVES 3
 #endif
-// Payload entries of one bucket's run, read 16 B at a time: the lanes of a
-// wave walk 64 different runs, so a 4-B load per step fetches 64 distinct
-// lines that are evicted (by the point loads) before the next step; an aligned
-// 4-entry window fetches each line once per 4 steps.  The payload buffer is
-// allocated with 64 B of slack, so a window past the last run's end stays in
-// bounds.
-struct PayloadWindow {
-  const uint4 *base;
-  uint4 w;
-  uint32_t pos;
-  MSM_FN PayloadWindow(const uint32_t *sorted, uint32_t off, uint32_t cnt)
-      : base(reinterpret_cast<const uint4 *>(sorted)), pos(off) {
-    if (cnt) w = base[off >> 2];
+// The entry stream of schedule position t (AccSched): row k of its wave
+// group's interleaved block (stride 64: one coalesced read per wave step), or,
+// for a group left in bucket order, its run in `sorted` (stride 1).
+struct PayloadStream {
+  const uint32_t *p;
+  uint32_t stride;
+  MSM_FN PayloadStream(const AccSched &S, uint32_t t) {
+    const uint32_t b = S.wbase[t >> 6];
+    if (b != ~0u) {
+      p = S.ipay + (size_t)b * 64 + (t & 63);
+      stride = 64;
+    } else {
+      p = S.sorted + S.offsets[t];
+      stride = 1;
+    }
   }
-  MSM_FN uint32_t next() {
-    const uint32_t q = pos & 3;
-    const uint32_t e = q == 0 ? w.x : q == 1 ? w.y : q == 2 ? w.z : w.w;
-    ++pos;
-    if ((pos & 3) == 0) w = base[pos >> 2];  // may read the slack after the run: unused
-    return e;
-  }
+  MSM_FN uint32_t at(uint32_t k) const { return p[(size_t)k * stride]; }
 };
 
 // One lane per bucket, buckets visited in the schedule `order` (descending
 // entry count, BucketSort) so the 64 lanes of a wave run loops of nearly equal
-// length and the longest buckets start first.  counts / offsets are indexed by
-// schedule position (BucketSort scnt / soff: coalesced); `order` gives the
-// bucket the sum is stored to.
+// length and the longest buckets start first.  Everything is read by schedule
+// position (AccSched: coalesced); S.order[t] is the bucket the sum is stored to.
 template <int G, class PT = Aff<typename FieldOf<G>::F>>
-__global__ void __launch_bounds__(256, MSM_ACC_WAVES) k_accumulate(const uint32_t *__restrict__ order,
-                                                    const uint32_t *__restrict__ counts,
-                                                    const uint32_t *__restrict__ offsets,
-                                                    const uint32_t *__restrict__ sorted,
-                                                    const PT *__restrict__ pts,
-                                                    Xyzz<typename FieldOf<G>::F> *__restrict__ buckets, size_t nbuckets) {
+__global__ void __launch_bounds__(256, MSM_ACC_WAVES)
+    k_accumulate(const AccSched S, const PT *__restrict__ pts, Xyzz<typename FieldOf<G>::F> *__restrict__ buckets,
+                 size_t nbuckets) {
   typedef typename FieldOf<G>::F F;
-  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= nbuckets) return;
-  const uint32_t cnt = counts[t];
-  PayloadWindow pw(sorted, offsets[t], cnt);
+  const uint32_t cnt = S.counts[t];
+  const PayloadStream ps(S, (uint32_t)t);
   Xyzz<F> acc;
   xyzz_set_inf(acc);
   for (uint32_t k = 0; k < cnt; ++k) {
-    const uint32_t e = pw.next();
+    const uint32_t e = ps.at(k);
     Aff<F> p = ld_point(&pts[e & 0x7fffffffu]);
     if (f_is_zero_exact(p.x) && f_is_zero_exact(p.y)) continue;  // affine infinity (ec_ops.h:717)
     xyzz_madd(acc, p, (e >> 31) != 0);
   }
-  st16(&buckets[order[t]], acc);
+  st16(&buckets[S.order[t]], acc);
 }
 
 // One level of the bucket reduction.  Invariant per window:

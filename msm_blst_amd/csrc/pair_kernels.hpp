@@ -45,26 +45,24 @@ __device__ __forceinline__ void st_xyzz2l(Xyzz<Fp2> *p, const Xyzz<Fp2L> &a, int
 
 // k_accumulate (kernels.hpp) for G2 with two lanes per bucket
 template <class PT>
-__global__ void __launch_bounds__(256) k_accumulate2p(const uint32_t *__restrict__ order,
-                                                      const uint32_t *__restrict__ counts,
-                                                      const uint32_t *__restrict__ offsets,
-                                                      const uint32_t *__restrict__ sorted, const PT *__restrict__ pts,
-                                                      Xyzz<Fp2> *__restrict__ buckets, size_t nbuckets) {
+__global__ void __launch_bounds__(256)
+    k_accumulate2p(const AccSched S, const PT *__restrict__ pts, Xyzz<Fp2> *__restrict__ buckets, size_t nbuckets) {
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= 2 * nbuckets) return;  // whole pairs only: 2 nbuckets lanes
   const int comp = (int)(t & 1);
-  const uint32_t cnt = counts[t >> 1];  // schedule-ordered (k_accumulate)
-  PayloadWindow pw(sorted, offsets[t >> 1], cnt);
+  const uint32_t pos = (uint32_t)(t >> 1);  // schedule position (k_accumulate)
+  const uint32_t cnt = S.counts[pos];
+  const PayloadStream ps(S, pos);
   Xyzz<Fp2L> acc;
   xyzz_set_inf(acc);
   for (uint32_t k = 0; k < cnt; ++k) {
-    const uint32_t e = pw.next();
+    const uint32_t e = ps.at(k);
     Aff<Fp2L> p;
     ld_point2l(p, &pts[e & 0x7fffffffu], comp);
     if (f_is_zero_exact(p.x) && f_is_zero_exact(p.y)) continue;  // affine infinity (ec_ops.h:717)
     xyzz_madd(acc, p, (e >> 31) != 0);
   }
-  st_xyzz2l(&buckets[order[t >> 1]], acc, comp);
+  st_xyzz2l(&buckets[S.order[pos]], acc, comp);
 }
 
 // k_segsum (ches_kernels.hpp) for G2 with two lanes per output
@@ -83,11 +81,21 @@ static __global__ void __launch_bounds__(256)
     xyzz_set_inf(acc);
   } else {
     ld_xyzz2l(acc, &src[idx ? idx[lo] : lo], comp);
+#if MSM_SEGSUM_PREFETCH
+    Xyzz<Fp2L> nxt;  // next operand loaded before the current add (k_segsum)
+    if (lo + 1 < hi) ld_xyzz2l(nxt, &src[idx ? idx[lo + 1] : lo + 1], comp);
+    for (uint32_t k = lo + 1; k < hi; ++k) {
+      Xyzz<Fp2L> a = nxt;
+      if (k + 1 < hi) ld_xyzz2l(nxt, &src[idx ? idx[k + 1] : k + 1], comp);
+      xyzz_add(acc, a);
+    }
+#else
     for (uint32_t k = lo + 1; k < hi; ++k) {
       Xyzz<Fp2L> a;
       ld_xyzz2l(a, &src[idx ? idx[k] : k], comp);
       xyzz_add(acc, a);
     }
+#endif
   }
   st_xyzz2l(&dst[o], acc, comp);
 }
@@ -124,15 +132,13 @@ static __global__ void __launch_bounds__(64)
 
 // ---- launchers (host) ----
 template <int G, class PT>
-inline void launch_accumulate(hipStream_t s, const uint32_t *order, const uint32_t *counts, const uint32_t *offsets,
-                              const uint32_t *sorted, const PT *pts, Xyzz<typename FieldOf<G>::F> *buckets, size_t nb) {
+inline void launch_accumulate(hipStream_t s, const AccSched &S, const PT *pts, Xyzz<typename FieldOf<G>::F> *buckets,
+                              size_t nb) {
   if (!nb) return;
   if constexpr (G == 1)
-    hipLaunchKernelGGL((k_accumulate<G, PT>), dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, order, counts, offsets, sorted, pts,
-                       buckets, nb);
+    hipLaunchKernelGGL((k_accumulate<G, PT>), dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, S, pts, buckets, nb);
   else
-    hipLaunchKernelGGL((k_accumulate2p<PT>), dim3((unsigned)((2 * nb + 255) / 256)), dim3(256), 0, s, order, counts, offsets, sorted,
-                       pts, buckets, nb);
+    hipLaunchKernelGGL((k_accumulate2p<PT>), dim3((unsigned)((2 * nb + 255) / 256)), dim3(256), 0, s, S, pts, buckets, nb);
 }
 // nmsm > 1: the same segment sums for nmsm MSMs of a batch group in one launch
 template <int G>

@@ -7,7 +7,12 @@
 #define MSM_FP_HOST_TEST 1
 #include <string.h>
 
+#include <condition_variable>
+#include <mutex>
+#include <thread>
+
 #include "../../msm_blst_amd/csrc/ec.hpp"
+#include "../../msm_blst_amd/csrc/fp2l.hpp"
 
 extern "C" {
 int msm_fp_overflow = 0;
@@ -67,6 +72,93 @@ void h_fp2_op(int op, uint32_t *r, const uint32_t *a, const uint32_t *b, const u
 }
 
 }  // extern "C"
+
+// ---- G2 lane pairs (fp2l.hpp): two threads in lockstep, lane 0 holds c0 and
+// lane 1 holds c1 of every Fp2 value; pair_swap is an exchange through two
+// double-buffered slots (a barrier per exchange) ----
+static thread_local int t_lane = 0;
+static std::mutex x_mu;
+static std::condition_variable x_cv;
+static uint32_t x_slot[2][2];
+static int x_arrived = 0;
+static uint64_t x_gen = 0;
+extern "C" int msm_host_lane(void) { return t_lane; }
+extern "C" uint32_t msm_host_pair_swap(uint32_t x) {
+  std::unique_lock<std::mutex> lk(x_mu);
+  const uint64_t my = x_gen;
+  x_slot[my & 1][t_lane] = x;
+  if (++x_arrived == 2) {
+    x_arrived = 0;
+    ++x_gen;
+    x_cv.notify_all();
+  } else {
+    x_cv.wait(lk, [&] { return x_gen != my; });
+  }
+  return x_slot[my & 1][t_lane ^ 1];
+}
+// run f(lane) on two lockstep threads
+template <class Fn>
+static void pair_run(Fn f) {
+  std::thread t0([&] { t_lane = 0; f(0); }), t1([&] { t_lane = 1; f(1); });
+  t0.join();
+  t1.join();
+}
+// component `lane` of the Fp2 values of an array of `count` Fp2 (c0 | c1 each)
+static void ldl(Fp2L *dst, const uint32_t *src, int count, int lane) {
+  for (int k = 0; k < count; ++k) memcpy(dst[k].c.v, src + (size_t)k * 2 * NL + lane * NL, NL * 4);
+}
+static void stl(uint32_t *dst, const Fp2L *src, int count, int lane) {
+  for (int k = 0; k < count; ++k) memcpy(dst + (size_t)k * 2 * NL + lane * NL, src[k].c.v, NL * 4);
+}
+// op codes as h_fp2_op
+extern "C" void h_fp2l_op(int op, uint32_t *r, const uint32_t *a, const uint32_t *b, const uint32_t *c,
+                          const uint32_t *d) {
+  pair_run([&](int lane) {
+    Fp2L A, B, C, D, R;
+    ldl(&A, a, 1, lane);
+    if (b) ldl(&B, b, 1, lane);
+    if (c) ldl(&C, c, 1, lane);
+    if (d) ldl(&D, d, 1, lane);
+    switch (op) {
+      case 0: f_mul(R, A, B); break;
+      case 1: f_sqr(R, A); break;
+      case 2: f_mul_bs(R, A, B); break;
+      case 3: f_mul_sub(R, A, B, C, D); break;
+      default: return;
+    }
+    stl(r, &R, 1, lane);
+  });
+}
+// xyzz formulas on lane pairs (ops as h_xyzz; acc: 4 Fp2, other: 2 (madd) or 4 Fp2)
+extern "C" void h_xyzz_l(int op, uint32_t *acc, const uint32_t *other, int neg) {
+  pair_run([&](int lane) {
+    Xyzz<Fp2L> A;
+    ldl(&A.x, acc, 1, lane);
+    ldl(&A.y, acc + 2 * NL, 1, lane);
+    ldl(&A.zzz, acc + 4 * NL, 1, lane);
+    ldl(&A.zz, acc + 6 * NL, 1, lane);
+    if (op == 0) {
+      Aff<Fp2L> p;
+      ldl(&p.x, other, 1, lane);
+      ldl(&p.y, other + 2 * NL, 1, lane);
+      xyzz_madd(A, p, neg != 0);
+    } else if (op == 1) {
+      Xyzz<Fp2L> B;
+      ldl(&B.x, other, 1, lane);
+      ldl(&B.y, other + 2 * NL, 1, lane);
+      ldl(&B.zzz, other + 4 * NL, 1, lane);
+      ldl(&B.zz, other + 6 * NL, 1, lane);
+      xyzz_add(A, B);
+    } else {
+      Xyzz<Fp2L> t = A;
+      xyzz_dbl(A, t);
+    }
+    stl(acc, &A.x, 1, lane);
+    stl(acc + 2 * NL, &A.y, 1, lane);
+    stl(acc + 4 * NL, &A.zzz, 1, lane);
+    stl(acc + 6 * NL, &A.zz, 1, lane);
+  });
+}
 
 // ---- xyzz formulas: op 0 madd(acc, P, neg), 1 add(acc, B), 2 dbl(acc) ----
 template <class F>

@@ -10,7 +10,9 @@ proven and then exercised at their bounds on the CPU (no GPU needed).
 2. The SAME header text (msm_blst_amd/csrc/fp.hpp, ec.hpp) is compiled for the
    host with every range check enabled (tests/host/fp_host_shim.cpp,
    MSM_FP_HOST_TEST) and run on max-limb operands of every range class and on
-   max-limb point coordinates, against Python big-integer arithmetic.
+   max-limb point coordinates, against Python big-integer arithmetic.  The
+   G2 lane-pair arithmetic (fp2l.hpp) runs the same way on two host threads in
+   lockstep standing in for the two lanes (pair_swap through the shim).
 """
 import ctypes
 import os
@@ -32,16 +34,19 @@ M28 = (1 << 28) - 1
 
 @pytest.fixture(scope="module")
 def shim():
-    deps = [SHIM_SRC] + [os.path.join(os.path.dirname(HERE), "msm_blst_amd", "csrc", f) for f in ("fp.hpp", "ec.hpp")]
+    deps = [SHIM_SRC] + [os.path.join(os.path.dirname(HERE), "msm_blst_amd", "csrc", f)
+                         for f in ("fp.hpp", "ec.hpp", "fp2l.hpp")]
     if not os.path.exists(SHIM_SO) or any(os.path.getmtime(d) > os.path.getmtime(SHIM_SO) for d in deps):
         os.makedirs(os.path.dirname(SHIM_SO), exist_ok=True)
-        subprocess.run(["g++", "-O1", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wno-unknown-pragmas", "-o",
-                        SHIM_SO, SHIM_SRC], check=True)
+        subprocess.run(["g++", "-O1", "-std=c++17", "-fPIC", "-shared", "-pthread", "-Wall", "-Wno-unknown-pragmas",
+                        "-o", SHIM_SO, SHIM_SRC], check=True)
     L = ctypes.CDLL(SHIM_SO)
     vp = ctypes.c_void_p
     L.h_fp_op.argtypes = [ctypes.c_int] + [vp] * 9
     L.h_fp2_op.argtypes = [ctypes.c_int] + [vp] * 5
     L.h_xyzz.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp, ctypes.c_int]
+    L.h_fp2l_op.argtypes = [ctypes.c_int] + [vp] * 5
+    L.h_xyzz_l.argtypes = [ctypes.c_int, vp, vp, ctypes.c_int]
     L.h_overflow.argtypes = [ctypes.c_int]
     return L
 
@@ -173,6 +178,31 @@ def test_fp2_primitives_at_class_bounds(shim, seed):
     assert (_val(list(r)[:NL]) % P, _val(list(r)[NL:]) % P) == ((ab[0] - cd[0]) % P, (ab[1] - cd[1]) % P)
 
 
+@pytest.mark.parametrize("seed", [None, 7, 8])
+def test_fp2l_lane_pair_primitives_at_class_bounds(shim, seed):
+    """fp2l.hpp's f_mul / f_sqr / f_mul_bs / f_mul_sub: each lane computes one
+    component from operands selected through pair_swap (its own products, e.g.
+    the odd lane's c1 = a0 (2 a1) in f_sqr), checked like the Fp2 versions."""
+    rnd = random.Random(seed) if seed is not None else None
+    S2 = _maxlimb(fb.S(), rnd) + _maxlimb(fb.S(), rnd)
+    lazy2 = _maxlimb(fb.sub(fb.S(), fb.S()), rnd) + _maxlimb(fb.sub(fb.S(), fb.S()), rnd)
+    lazy18 = _maxlimb(fb.sub(fb.S(), fb.Xc(), 16), rnd) + _maxlimb(fb.sub(fb.S(), fb.Xc(), 16), rnd)
+    shim.h_overflow(1)
+    for op, a, b in ((0, lazy2, lazy2), (1, lazy2, lazy2), (2, lazy2, S2), (1, lazy18, lazy18), (2, lazy18, S2)):
+        r = (ctypes.c_uint32 * (2 * NL))()
+        shim.h_fp2l_op(op, r, _arr(a), _arr(b), None, None)
+        assert shim.h_overflow(1) == 0, op
+        r = list(r)
+        assert all(x <= M28 for x in r[:NL - 1] + r[NL:2 * NL - 1]), op
+        assert _val(r[:NL]) < 2 * P and _val(r[NL:]) < 2 * P, op
+        assert (_val(r[:NL]) % P, _val(r[NL:]) % P) == _fp2_mont(a, a if op == 1 else b), op
+    r = (ctypes.c_uint32 * (2 * NL))()
+    shim.h_fp2l_op(3, r, _arr(lazy2), _arr(lazy2), _arr(S2), _arr(S2))
+    assert shim.h_overflow(1) == 0
+    ab, cd = _fp2_mont(lazy2, lazy2), _fp2_mont(S2, S2)
+    assert (_val(list(r)[:NL]) % P, _val(list(r)[NL:]) % P) == ((ab[0] - cd[0]) % P, (ab[1] - cd[1]) % P)
+
+
 # ---- the xyzz formulas on max-limb coordinates vs the same algebra mod p ----
 class _F:
     """Montgomery-domain field algebra mod p (R = 2^392) for G1 (ints) / G2 (pairs)"""
@@ -290,4 +320,34 @@ def test_xyzz_formulas_at_class_bounds(shim, group, seed):
             want = _ref_add(F, dec(acc), dec(oth))
         else:
             want = _ref_dbl(F, dec(acc))
+        assert dec(coords) == want, (op, neg)
+
+
+@pytest.mark.parametrize("seed", [None, 21, 22])
+def test_xyzz_lane_pair_formulas_at_class_bounds(shim, seed):
+    """ec.hpp's madd / add / dbl on Fp2L (the G2 accumulation and reduction
+    kernels' arithmetic), two lockstep host threads as the lane pair."""
+    group = 2
+    rnd = random.Random(seed) if seed is not None else None
+    F = _F(group)
+    W = NL * group
+    r2 = rnd or random.Random(96)
+    acc = [_elem(group, rnd, fb.Xc())] + [_elem(group, r2, fb.S()) for _ in range(3)]
+    r3 = rnd or random.Random(97)
+    oth = [_elem(group, r3, fb.Xc())] + [_elem(group, r3, fb.S()) for _ in range(3)]
+    pt = [_elem(group, rnd, fb.canonical()) for _ in range(2)]
+    dec = lambda ws: tuple(_dec(group, w) for w in ws)  # noqa: E731
+    shim.h_overflow(1)
+    for op, neg in ((0, 0), (0, 1), (1, 0), (2, 0)):
+        a = _arr(sum(acc, []))
+        other = _arr(sum(pt if op == 0 else oth, []))
+        shim.h_xyzz_l(op, a, other, neg)
+        assert shim.h_overflow(1) == 0, (op, neg)
+        out = list(a)
+        coords = [out[k * W:(k + 1) * W] for k in range(4)]
+        _check_S(group, coords[0], 10)
+        for c in coords[1:]:
+            _check_S(group, c)
+        want = (_ref_madd(F, dec(acc), dec(pt), neg) if op == 0 else
+                _ref_add(F, dec(acc), dec(oth)) if op == 1 else _ref_dbl(F, dec(acc)))
         assert dec(coords) == want, (op, neg)

@@ -95,6 +95,27 @@ def test_equal_points_doubling_branch(m):
     ctx.close()
 
 
+@pytest.mark.parametrize("group,n_exp", [(1, 16), (2, 12)])
+def test_skewed_buckets_mixed_payload_layout(m, group, n_exp):
+    """A quarter of the scalars equal: their digits pile into h buckets of n/4
+    entries each, whose wave groups keep the bucket-ordered payload (padding
+    would exceed 2x), beside interleaved groups of ordinary buckets
+    (bucket_sort.hpp k_wave_len / k_interleave) -- vs the CPU oracle."""
+    n = 1 << n_exp
+    pts = bytes(m.fixed_points(group, n))
+    sc = bytearray(bytes(m.gen_scalars(n, 11)))
+    same = bytes(m.gen_scalars(1, 12))
+    for i in range(0, n, 4):
+        sc[32 * i:32 * i + 32] = same
+    ctx = m.CHESContext(group, 0, n_exp=n_exp)
+    ctx.build_table(pts, n)
+    got = m.compress(group, ctx.mult(bytes(sc)))
+    ctx.close()
+    cp = (ctypes.c_uint8 * len(pts)).from_buffer_copy(pts)
+    cs = (ctypes.c_uint8 * len(sc)).from_buffer_copy(bytes(sc))
+    assert got.hex() == of.compress(group, of.msm(group, cp, cs, n, 255, "pippenger"))
+
+
 @pytest.mark.parametrize("n_exp", [16, 20])
 def test_ches_g1_large_vs_reference(m, golden, points, n_exp):
     n = 1 << n_exp

@@ -37,12 +37,12 @@ if sys.argv[4] == "20" and sys.argv[3] == "ches":
     out["decomposition_bytes"] = {
         "table_rows_128B_lines": n * h * 128,          # 112-B internal rows padded to one 128-B line
         "table_rows_blst_96B_algorithmic": n * h * 96,
-        "sorted_payload_4B": n * h * 4,
-        "bucket_meta_order_counts_offsets": nb * 12,
+        "payload_4B": n * h * 4,                       # interleaved rows: one coalesced 256-B read per wave step
+        "schedule_order_counts_offsets_wave_rows": nb * 12 + (nb // 64) * 8,
         "bucket_xyzz_writes_224B": nb * 224,
-        "note": "counts[id]/offsets[id] are random 4-B reads and each bucket's payload run spans 1-2 lines: at "
-                "line granularity these add up to ~0.4 GB more; the rest of the FETCH excess is uncalibrated "
-                "(small random reads)"}
+        "note": "round 3: counts/offsets are read by schedule position (coalesced) and the payload from "
+                "per-wave interleaved rows (bucket_sort.hpp k_interleave); before, counts[id]/offsets[id] "
+                "were random 4-B reads and each lane's payload run was re-fetched per step (2.63 GB/launch)"}
 if len(sys.argv) > 6:
     out["calibration"] = json.load(open(sys.argv[6]))
 js = json.dumps(out, indent=1)
