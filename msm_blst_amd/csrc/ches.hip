@@ -786,7 +786,11 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
   for (int f = 0; f < kFronts; ++f) unsized |= fs_[f].sorted.bytes < n * (size_t)p_.h * fg_max * 4;
   // host sets: nsg groups of fg_max device slots, copied up to nsg groups ahead
   // (4 single-set groups -- as the round-2 pipeline's four slots -- or 2 larger)
-  const size_t nsg = fg_max == 1 ? 4 : 2;
+  static const size_t nsg_env = [] {
+    const char *e = getenv("MSM_H2D_SLOTS");  // A/B knob: slot groups (copies issued that far ahead)
+    return (size_t)(e ? std::max(2, std::min(256, atoi(e))) : 0);
+  }();
+  const size_t nsg = nsg_env ? nsg_env : fg_max == 1 ? 4 : 2;
   if (scalars_on_host || unsized) scal_.ensure(std::max<size_t>(nsg, 2) * fg_max * sslot + 16);
   for (int f = 0; f < kFronts; ++f)
     if (fs_[f].sorted.bytes < n * (size_t)p_.h * fg_max * 4) {

@@ -63,12 +63,17 @@ MSM_FN void xyzz_dbl(Xyzz<F> &r, const Xyzz<F> &a) {
     r = a;
     return;
   }
-  F U, V, W, S, M, t, X3, Y3;
+  // ordered so that each input coordinate dies at its last use (r may alias a):
+  // at most 7 field elements live, as in the madd -- this branch sits inside
+  // the accumulation loop, so its peak sets the kernel's VGPR count
+  F U, V, W, S, M, t, X3;
   f_add(U, a.y, a.y);      // < 4p lazy
   f_sqr(V, U);             // S
   f_mul(W, V, U);          // S
   f_mul(S, a.x, V);        // S
-  f_sqr(M, a.x);           // S
+  f_mul(r.zz, V, a.zz);    // ZZ3 = V ZZ (V, ZZ die)
+  f_mul(r.zzz, W, a.zzz);  // ZZZ3 = W ZZZ
+  f_sqr(M, a.x);           // S (X dies)
   f_mul3(M, M);            // < 6p lazy
   f_sqr(X3, M);            // S
   F z;
@@ -76,11 +81,8 @@ MSM_FN void xyzz_dbl(Xyzz<F> &r, const Xyzz<F> &a) {
   f_sub_2x(X3, X3, z, S);  // M^2 + 8p - 2S   < 10p
   f_norm(X3);              // X
   f_sub16(t, S, X3);       // < 18p
-  f_mul_sub(Y3, t, M, W, a.y);  // M (S - X3) - W Y   S (one reduction)
-  f_mul(r.zz, V, a.zz);
-  f_mul(r.zzz, W, a.zzz);
+  f_mul_sub(r.y, t, M, W, a.y);  // Y3 = M (S - X3) - W Y   S (one reduction)
   r.x = X3;
-  r.y = Y3;
 }
 
 // acc += (neg ? -P : P); P affine, canonical, not infinity (callers skip the
@@ -103,12 +105,14 @@ MSM_FN void xyzz_madd(Xyzz<F> &acc, const Aff<F> &p, bool neg) {
   f_sub4(R, R, acc.y);     // R = S2 - Y1          < 6p lazy
   f_sqr(PP, P);            // PP                   S
   if (__builtin_expect(f_is_zero_S(PP), 0)) {
-    // X1 == X2: either P == bucket (double P) or P == -bucket (infinity)
+    // X1 == X2: either P == bucket (double it) or P == -bucket (infinity)
     F RR;
     f_sqr(RR, R);
     if (f_is_zero_S(RR)) {
-      Xyzz<F> b;
-      xyzz_from_aff(b, p, neg);
+      // +-P equals the bucket: double the bucket itself (still untouched
+      // here), so the affine operand dies after U2 and S2 instead of staying
+      // live through the whole madd for this branch
+      Xyzz<F> b = acc;
       xyzz_dbl(acc, b);
     } else {
       xyzz_set_inf(acc);

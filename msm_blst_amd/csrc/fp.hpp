@@ -198,19 +198,27 @@ MSM_FN void fp_mul4(Fp &r, const Fp &a, const Fp &b, const Fp &c, const Fp &d, c
   r.v[NL - 1] = top32(acc);
 }
 
-// Montgomery square: cross products once, doubled (limbs < 2^29 so 2a_i < 2^30).
+// doubled cross sum of a square column folded into the accumulator: acc + 2x
+// in one v_lshl_add_u64 (x is its own mad chain, so the column keeps two
+// independent chains without a doubled copy of the operand)
+MSM_FN uint64_t add_dbl(uint64_t x, uint64_t acc) {
+  MSM_CHECK(x < (1ull << 63) && (x << 1) <= ~acc);
+  return (x << 1) + acc;
+}
+// Montgomery square: each cross product once, per column x = sum_{i<j} a_i a_j
+// on its own chain and acc += 2x (no doubled operand copy: 14 fewer live
+// VGPRs and 14 fewer shifts than squaring against a << 1).
 MSM_FN void fp_sqr(Fp &r, const Fp &a) {
-  uint32_t m[NL], a2[NL];
-#pragma unroll
-  for (int i = 0; i < NL; ++i) {
-    MSM_CHECK(a.v[i] < 0x80000000u);
-    a2[i] = a.v[i] << 1;
-  }
+  uint32_t m[NL];
   uint64_t acc = 0;
 #pragma unroll
   for (int k = 0; k < NL; ++k) {
+    if (k > 0) {
+      uint64_t x = 0;
 #pragma unroll
-    for (int i = 0; 2 * i < k; ++i) acc = mad64(a2[i], a.v[k - i], acc);
+      for (int i = 0; 2 * i < k; ++i) x = mad64(a.v[i], a.v[k - i], x);
+      acc = add_dbl(x, acc);
+    }
     if ((k & 1) == 0) acc = mad64(a.v[k / 2], a.v[k / 2], acc);
 #pragma unroll
     for (int i = 0; i < k; ++i) acc = mad64(m[i], P28[k - i], acc);
@@ -220,8 +228,12 @@ MSM_FN void fp_sqr(Fp &r, const Fp &a) {
   }
 #pragma unroll
   for (int k = NL; k < 2 * NL - 1; ++k) {
+    if (k < 2 * NL - 2) {
+      uint64_t x = 0;
 #pragma unroll
-    for (int i = k - NL + 1; 2 * i < k; ++i) acc = mad64(a2[i], a.v[k - i], acc);
+      for (int i = k - NL + 1; 2 * i < k; ++i) x = mad64(a.v[i], a.v[k - i], x);
+      acc = add_dbl(x, acc);
+    }
     if ((k & 1) == 0) acc = mad64(a.v[k / 2], a.v[k / 2], acc);
 #pragma unroll
     for (int i = k - NL + 1; i < NL; ++i) acc = mad64(m[i], P28[k - i], acc);

@@ -137,19 +137,26 @@ def mul4(a, b, c, d, e, f, g, h):
 
 
 def sqr(a):
-    """fp_sqr: cross products once with the doubled operand a2 = a << 1"""
-    need(all(l < (1 << 31) for l in a.lim), "fp_sqr: a << 1 wraps")
-    a2 = [2 * l for l in a.lim]
+    """fp_sqr: per column the cross products once on their own chain x, then
+    acc += 2x (add_dbl: x < 2^63 and 2x + acc < 2^64)"""
     acc, m, out = 0, M - 1, [0] * NL
+
+    def cross(k, lo):
+        x = sum(a.lim[i] * a.lim[k - i] for i in range(lo, NL) if 2 * i < k and k - i < NL)
+        need(x < (1 << 63), f"fp_sqr: column {k} cross sum {x.bit_length()} bits")
+        return 2 * x
+
     for k in range(NL):
-        acc += sum(a2[i] * a.lim[k - i] for i in range(k + 1) if 2 * i < k)
+        acc += cross(k, 0)
+        need(acc < U64, f"fp_sqr: column {k} after 2x")
         if k % 2 == 0:
             acc += a.lim[k // 2] ** 2
         acc += sum(m * P28[k - i] for i in range(k)) + m * P28[0]
         need(acc < U64, f"fp_sqr: column {k}")
         acc >>= 28
     for k in range(NL, 2 * NL - 1):
-        acc += sum(a2[i] * a.lim[k - i] for i in range(k - NL + 1, NL) if 2 * i < k)
+        acc += cross(k, k - NL + 1)
+        need(acc < U64, f"fp_sqr: column {k} after 2x")
         if k % 2 == 0:
             acc += a.lim[k // 2] ** 2
         acc += sum(m * P28[k - i] for i in range(k - NL + 1, NL))
@@ -331,10 +338,8 @@ def trace_madd(group, negate):
     X3 = _x3(F, Rd, PPP, Q)
     t = sub(Q, X3, 16)
     Y3 = F.mul_sub(t, Rd, y, PPP)
-    # doubling branch: b = xyzz_from_aff(P, neg) (y negated then nred, ZZ = ZZZ = one), then dbl
-    by = nred(neg(py)) if negate else py
-    one = canonical()
-    dbl = trace_dbl(group, (px, by, one, one))
+    # doubling branch (+-P equals the bucket): the untouched bucket itself is doubled
+    dbl = trace_dbl(group, (x, y, zzz, zz))
     return (X3, Y3, zzz3, zz3), dbl
 
 
