@@ -233,7 +233,11 @@ void WeightedReducer<G>::plan(const std::vector<uint32_t> &w, const std::vector<
   }
   // level 0 + pairwise levels
   std::vector<uint32_t> cur_seg = seg;
-  int C = 8;
+  static const int C0 = [] {
+    const char *e = getenv("MSM_L0_CHUNK");  // A/B knob: level-0 chunk length
+    return e ? std::max(2, std::min(64, atoi(e))) : 8;
+  }();
+  int C = C0;
   while (true) {
     std::vector<uint32_t> st, nseg;
     size_t k = 0;

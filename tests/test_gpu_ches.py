@@ -168,11 +168,11 @@ def test_mult_batch_matches_single(m, golden):
 @pytest.mark.parametrize("group,log_n,K", [(1, 16, 7), (2, 10, 7), (1, 12, 9), (1, 12, 17), (2, 10, 9),
                                            (2, 10, 17)])
 def test_mult_batch_sets_resident_and_pinned(m, group, log_n, K):
-    """Batches longer than every ring (Ches: front groups ramping 1, 1, 2, 4, 8 MSMs,
-    in kFronts = 2 alternating front sets; kBSets = 2 bucket
-    sets; host sets in 2 x 8 device slots copied on their own stream): K distinct
-    sets from device memory and from page-locked host memory (streamed group by
-    group inside the pipeline) equal the synchronous MSMs.  K = 9 and 17 also
+    """Batches longer than every ring (Ches::run_batch: single-set front groups in
+    kFronts = 3 rotating front sets; kBSets = 2 bucket sets; host sets in 4
+    device slots copied on their own stream, cstream_): K distinct sets from
+    device memory and from page-locked host memory (streamed set by set inside
+    the pipeline) equal the synchronous MSMs.  K = 9 and 17 also
     exceed one reduction group (kGroup = 8): several groups of uneven size R
     alternate between the two reducer buffer sets / tail streams and read back
     at their own offsets, and the front groups (1, 1, 2, 4, 8, ...) straddle them."""
