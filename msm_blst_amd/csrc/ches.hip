@@ -643,12 +643,51 @@ void Ches<G>::digits_sort(hipStream_t s, const uint8_t *d_scalars, size_t stride
                           int set) {
   const size_t n = n_, h = (size_t)p_.h, ne = n * h, NB = bucket_count();
   ChesFrontSet &f = fs_[set];
-  f.keys.ensure(ne * nsets * 4);
-  f.vals.ensure(ne * nsets * 4);
   f.sorted.ensure(ne * nsets * 4 + 64);  // + the accumulation's 16-B payload window past a run's end
   f.counts.ensure(NB * nsets * 4);
   f.offsets.ensure(NB * nsets * 4);
   f.order.ensure(NB * nsets * 4);
+  // Fused front (the h of every reference configuration): the digits are
+  // computed twice -- counted per coarse bin, then binned -- instead of being
+  // written as keys / vals and read back twice by the sort (5 launches after
+  // the scan's 2 instead of 8; MSM_FRONT_FUSED=0 selects the unfused front)
+  static const bool fused_env = [] {
+    const char *e = getenv("MSM_FRONT_FUSED");
+    return !e || atoi(e) != 0;
+  }();
+  if (fused_env && (p_.h == 12 || p_.h == 13 || p_.h == 14 || p_.h == 16 || p_.h == 19 || p_.h == 20)) {
+    const int ntiles = (int)nblk(n, 256);
+    const BucketSort::Geom g = f.sort.prepare(s, ne, (uint32_t)NB, nsets, ntiles);
+#define MSM_CHES_FRONT(HT)                                                                                             \
+  do {                                                                                                                 \
+    hipLaunchKernelGGL(k_ches_front_hist<HT>, dim3(ntiles, nsets), dim3(256), 0, s, d_scalars, stride, n, p_.q_exp,   \
+                       code_.as<uint32_t>(), rank_.as<uint2>(), (uint32_t)B_.size(), (uint32_t)small_,                 \
+                       (uint32_t)copies_, set_stride, g.fb_bits, g.ncb, g.ntiles, f.sort.ghist.as<uint32_t>(),         \
+                       f.sort.classes.as<uint32_t>());                                                                  \
+    MSM_HIP_CHECK(hipGetLastError());                                                                                  \
+    if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[1], s));                                                            \
+    f.sort.scan(s, g);                                                                                                 \
+    hipLaunchKernelGGL(k_ches_front_coarse<HT>, dim3(ntiles, nsets), dim3(256), (size_t)(2 * g.ncb + 512 * HT) * 4, s, \
+                       d_scalars, stride, n, p_.q_exp, code_.as<uint32_t>(), rank_.as<uint2>(), (uint32_t)B_.size(),  \
+                       (uint32_t)small_, (uint32_t)copies_, set_stride, g.fb_bits, g.ncb, g.ntiles,                   \
+                       f.sort.gbase.as<uint32_t>(), f.sort.okeys.as<uint32_t>(), f.sort.ovals.as<uint32_t>());         \
+    MSM_HIP_CHECK(hipGetLastError());                                                                                  \
+  } while (0)
+    switch (p_.h) {
+      case 12: MSM_CHES_FRONT(12); break;
+      case 13: MSM_CHES_FRONT(13); break;
+      case 14: MSM_CHES_FRONT(14); break;
+      case 16: MSM_CHES_FRONT(16); break;
+      case 19: MSM_CHES_FRONT(19); break;
+      default: MSM_CHES_FRONT(20); break;
+    }
+#undef MSM_CHES_FRONT
+    f.sort.finish(s, g, ne, (uint32_t)NB, f.sorted.as<uint32_t>(), f.counts.as<uint32_t>(), f.offsets.as<uint32_t>(),
+                  f.order.as<uint32_t>(), nsets);
+    return;
+  }
+  f.keys.ensure(ne * nsets * 4);
+  f.vals.ensure(ne * nsets * 4);
 #define MSM_CHES_DIGITS(HT)                                                                                   \
   hipLaunchKernelGGL(k_ches_digits<HT>, dim3(nblk(n, 256), nsets), dim3(256), 0, s, d_scalars, stride, n, p_.q_exp, \
                      p_.h, code_.as<uint32_t>(), rank_.as<uint2>(), f.keys.as<uint32_t>(), f.vals.as<uint32_t>(),     \

@@ -17,6 +17,7 @@
 // Bucket accumulation and the dense window reduction reuse k_accumulate /
 // k_reduce of kernels.hpp.
 #pragma once
+#include "bucket_sort.hpp"
 #include "kernels.hpp"
 
 namespace msm {
@@ -296,6 +297,143 @@ static __global__ void __launch_bounds__(256)
       carry = (c >> 2) & 1u;
       emit(j, entry(c, b));
     }
+  }
+}
+
+// ------------------------------------------------ fused CHES front (HT > 0) --
+// The h entries of scalar i as k_ches_digits computes them (key = bucket or
+// KEY_NONE, val = table slot | sign << 31), kept in registers.
+template <int HT>
+__device__ __forceinline__ void ches_entries(const uint8_t *__restrict__ sp, size_t stride, size_t i, int q_exp,
+                                             const uint32_t *__restrict__ code, const uint2 *__restrict__ rank,
+                                             uint32_t nb0, uint32_t small, uint32_t copies, uint32_t (&key)[HT],
+                                             uint32_t (&val)[HT]) {
+  uint32_t s[10];
+  if ((stride & 3) == 0) {
+    const uint32_t *s32 = reinterpret_cast<const uint32_t *>(sp);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s[k] = s32[k];
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      s[k] = (uint32_t)sp[4 * k] | ((uint32_t)sp[4 * k + 1] << 8) | ((uint32_t)sp[4 * k + 2] << 16) |
+             ((uint32_t)sp[4 * k + 3] << 24);
+  }
+  sub_r_if_ge(s);
+  sub_r_if_ge(s);
+  s[8] = s[9] = 0;
+  const uint32_t qmask = (1u << q_exp) - 1u, q = 1u << q_exp;
+  uint32_t dj[HT], cj[HT];
+#pragma unroll
+  for (int j = 0; j < HT; ++j) {
+    const int off = j * q_exp, wi = off >> 5, sh = off & 31;
+    const uint32_t lo = wi < 10 ? s[wi] : 0u, hi = wi + 1 < 10 ? s[wi + 1] : 0u;
+    dj[j] = (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) & qmask;
+    const uint2 w = *reinterpret_cast<const uint2 *>(code + (dj[j] >> 3));  // code pair (d, d + 1)
+    cj[j] = (uint32_t)(((((uint64_t)w.y << 32) | w.x) >> (4 * (dj[j] & 7))) & 0xffu);
+  }
+  uint32_t carry = 0;
+#pragma unroll
+  for (int j = 0; j < HT; ++j) {
+    const uint32_t c = carry ? cj[j] >> 4 : cj[j] & 15u, d = dj[j] + carry;
+    const uint32_t m1 = c & 3u, v = (c & 4u) ? q - d : d;
+    dj[j] = m1 == 0 ? v : (m1 == 1 ? v >> 1 : v / 3u);  // bucket value b
+    cj[j] = c;
+    carry = (c >> 2) & 1u;
+  }
+#pragma unroll
+  for (int j = 0; j < HT; ++j) {
+    const uint32_t c = cj[j];
+    uint32_t b = 0;
+    if (!(c & 8u)) {
+      const uint2 r = rank[dj[j] >> 5];
+      b = r.y + (uint32_t)__popc(r.x & ((1u << (dj[j] & 31)) - 1u));
+    }
+    if (j == HT - 1 && b != 0 && b <= small) {
+      const uint32_t cp = (uint32_t)(i % copies);
+      if (cp) b = nb0 + (cp - 1) * small + b - 1;
+    }
+    key[j] = b ? b : KEY_NONE;
+    val[j] = (uint32_t)(3 * (i * (size_t)HT + j) + (c & 3u)) | ((c & 4u) << 29);
+  }
+}
+
+// Front pass A: the digits of a tile of 256 scalars (256 HT entries) counted
+// per coarse bin in LDS -> ghist[set][bin][tile] (bucket_sort.hpp k_bs_hist
+// without the keys array: nothing is written per entry).  Block 0 clears the
+// schedule's class counters.
+template <int HT>
+static __global__ void __launch_bounds__(256)
+    k_ches_front_hist(const uint8_t *__restrict__ scalars, size_t stride, size_t n, int q_exp,
+                      const uint32_t *__restrict__ code, const uint2 *__restrict__ rank, uint32_t nb0, uint32_t small,
+                      uint32_t copies, size_t set_stride, int fb_bits, int ncb, int ntiles, uint32_t *__restrict__ ghist,
+                      uint32_t *__restrict__ classes) {
+  __shared__ uint32_t h[BS_MAX_CB];
+  scalars += (size_t)blockIdx.y * set_stride;
+  ghist += (size_t)blockIdx.y * ncb * ntiles;
+  if (blockIdx.x == 0)
+    for (int c = threadIdx.x; c < 512; c += blockDim.x) classes[(size_t)blockIdx.y * 512 + c] = 0;
+  for (int b = threadIdx.x; b < ncb; b += blockDim.x) h[b] = 0;
+  __syncthreads();
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    uint32_t key[HT], val[HT];
+    ches_entries<HT>(scalars + i * stride, stride, i, q_exp, code, rank, nb0, small, copies, key, val);
+#pragma unroll
+    for (int j = 0; j < HT; ++j)
+      if (key[j] != KEY_NONE) atomicAdd(&h[key[j] >> fb_bits], 1u);
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < ncb; b += blockDim.x) ghist[(size_t)b * ntiles + blockIdx.x] = h[b];
+}
+
+// Front pass B: the same digits recomputed, ranked per coarse bin in LDS and
+// staged bin-sorted in LDS, then streamed to the tile's run of each bin
+// (k_bs_coarse with the entries taken from registers instead of keys / vals
+// arrays: the digit kernel's 8-B-per-entry write and the sort's two reads of
+// it are gone).  gbase: exclusive scan of ghist.  Dynamic LDS: 2 ncb + 2 * 256 HT words.
+template <int HT>
+static __global__ void __launch_bounds__(256)
+    k_ches_front_coarse(const uint8_t *__restrict__ scalars, size_t stride, size_t n, int q_exp,
+                        const uint32_t *__restrict__ code, const uint2 *__restrict__ rank, uint32_t nb0,
+                        uint32_t small, uint32_t copies, size_t set_stride, int fb_bits, int ncb, int ntiles,
+                        const uint32_t *__restrict__ gbase, uint32_t *__restrict__ okeys,
+                        uint32_t *__restrict__ ovals) {
+  extern __shared__ uint32_t sm[];
+  __shared__ uint32_t wsum[4];
+  uint32_t *loff = sm, *gb = sm + ncb, *sk = sm + 2 * ncb, *sv = sk + 256 * HT;
+  scalars += (size_t)blockIdx.y * set_stride;
+  gbase += (size_t)blockIdx.y * ncb * ntiles;
+  for (int b = threadIdx.x; b < ncb; b += blockDim.x) {
+    loff[b] = 0;
+    gb[b] = gbase[(size_t)b * ntiles + blockIdx.x];
+  }
+  __syncthreads();
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t key[HT], val[HT], rk[HT];
+  if (i < n) {
+    ches_entries<HT>(scalars + i * stride, stride, i, q_exp, code, rank, nb0, small, copies, key, val);
+  } else {
+#pragma unroll
+    for (int j = 0; j < HT; ++j) key[j] = KEY_NONE, val[j] = 0;
+  }
+#pragma unroll
+  for (int j = 0; j < HT; ++j) rk[j] = key[j] != KEY_NONE ? atomicAdd(&loff[key[j] >> fb_bits], 1u) : 0u;
+  __syncthreads();
+  const uint32_t total = block_exclusive_scan_256(loff, ncb, wsum);
+#pragma unroll
+  for (int j = 0; j < HT; ++j) {
+    if (key[j] == KEY_NONE) continue;
+    const uint32_t pos = loff[key[j] >> fb_bits] + rk[j];
+    sk[pos] = key[j];
+    sv[pos] = val[j];
+  }
+  __syncthreads();
+  for (uint32_t e = threadIdx.x; e < total; e += 256) {
+    const uint32_t k = sk[e], b = k >> fb_bits;
+    const uint32_t g = gb[b] + (e - loff[b]);
+    okeys[g] = k;
+    ovals[g] = sv[e];
   }
 }
 

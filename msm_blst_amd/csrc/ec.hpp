@@ -63,17 +63,12 @@ MSM_FN void xyzz_dbl(Xyzz<F> &r, const Xyzz<F> &a) {
     r = a;
     return;
   }
-  // ordered so that each input coordinate dies at its last use (r may alias a):
-  // at most 7 field elements live, as in the madd -- this branch sits inside
-  // the accumulation loop, so its peak sets the kernel's VGPR count
-  F U, V, W, S, M, t, X3;
+  F U, V, W, S, M, t, X3, Y3;
   f_add(U, a.y, a.y);      // < 4p lazy
   f_sqr(V, U);             // S
   f_mul(W, V, U);          // S
   f_mul(S, a.x, V);        // S
-  f_mul(r.zz, V, a.zz);    // ZZ3 = V ZZ (V, ZZ die)
-  f_mul(r.zzz, W, a.zzz);  // ZZZ3 = W ZZZ
-  f_sqr(M, a.x);           // S (X dies)
+  f_sqr(M, a.x);           // S
   f_mul3(M, M);            // < 6p lazy
   f_sqr(X3, M);            // S
   F z;
@@ -81,7 +76,10 @@ MSM_FN void xyzz_dbl(Xyzz<F> &r, const Xyzz<F> &a) {
   f_sub_2x(X3, X3, z, S);  // M^2 + 8p - 2S   < 10p
   f_norm(X3);              // X
   f_sub16(t, S, X3);       // < 18p
-  f_mul_sub(r.y, t, M, W, a.y);  // Y3 = M (S - X3) - W Y   S (one reduction)
+  f_mul_sub(Y3, t, M, W, a.y);  // M (S - X3) - W Y   S (one reduction)
+  f_mul(r.zz, V, a.zz);
+  f_mul(r.zzz, W, a.zzz);
+  r.y = Y3;
   r.x = X3;
 }
 

@@ -20,44 +20,64 @@
 namespace msm {
 
 #if MSM_GROUP == 1  // group-independent: compiled once
-void BucketSort::run(hipStream_t s, const uint32_t *keys, const uint32_t *vals, size_t ne, uint32_t nb,
-                     uint32_t *sorted, uint32_t *counts, uint32_t *offsets, uint32_t *order, int nsets) {
+BucketSort::Geom BucketSort::prepare(hipStream_t s, size_t ne, uint32_t nb, int nsets, int ntiles) {
   // ~256 coarse bins (see bucket_sort.hpp), fine buckets per bin in [2^8, 2^12]
-  int fb_bits = 8;
-  while (fb_bits < BS_MAX_FB_BITS && ((size_t)nb >> fb_bits) > 384) ++fb_bits;
-  const int ncb = (int)(((size_t)nb + (1u << fb_bits) - 1) >> fb_bits);
-  if (ncb > BS_MAX_CB || ncb > 4096) throw std::runtime_error("BucketSort: too many buckets");
+  Geom g;
+  g.fb_bits = 8;
+  while (g.fb_bits < BS_MAX_FB_BITS && ((size_t)nb >> g.fb_bits) > 384) ++g.fb_bits;
+  g.ncb = (int)(((size_t)nb + (1u << g.fb_bits) - 1) >> g.fb_bits);
+  if (g.ncb > BS_MAX_CB || g.ncb > 4096) throw std::runtime_error("BucketSort: too many buckets");
   if (nsets < 1 || nsets > 65535) throw std::runtime_error("BucketSort: bad set count");
   if (ne * nsets >= (1ull << 32)) throw std::runtime_error("BucketSort: too many entries");
-  const int ntiles = (int)std::max<size_t>(1, (ne + BS_TILE - 1) / BS_TILE);
-  const size_t nslots = (size_t)nsets * ncb * ntiles;
-  if (nslots >= (1ull << 31)) throw std::runtime_error("BucketSort: too many histogram slots");
-  ghist.ensure(nslots * 4);
-  gbase.ensure(nslots * 4);
+  g.ntiles = ntiles > 0 ? ntiles : (int)std::max<size_t>(1, (ne + BS_TILE - 1) / BS_TILE);
+  g.nslots = (size_t)nsets * g.ncb * g.ntiles;
+  if (g.nslots >= (1ull << 31)) throw std::runtime_error("BucketSort: too many histogram slots");
+  ghist.ensure(g.nslots * 4);
+  gbase.ensure(g.nslots * 4);
   okeys.ensure(std::max<size_t>(ne * nsets, 1) * 4);
   ovals.ensure(std::max<size_t>(ne * nsets, 1) * 4);
-  const size_t nw = groups(nb);
-  wbase.ensure(nw * nsets * 4);
+  wbase.ensure(groups(nb) * nsets * 4);
   ipay_stride = ne + BS_IPAY_SLACK;
   ipay.ensure(ipay_stride * nsets * 4);
   size_t scan_tmp = 0;
-  hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, ghist.as<uint32_t>(), gbase.as<uint32_t>(), (int)nslots, s);
+  hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, ghist.as<uint32_t>(), gbase.as<uint32_t>(), (int)g.nslots, s);
   tmp.ensure(scan_tmp);
-  classes.ensure((size_t)512 * 4 * nsets);  // per set: 256 class totals + 256 cursors, cleared by k_bs_hist
-  hipLaunchKernelGGL(k_bs_hist, dim3(ntiles, nsets), dim3(256), 0, s, keys, ne, fb_bits, ncb, ntiles,
+  g.scan_tmp = scan_tmp;
+  classes.ensure((size_t)512 * 4 * nsets);  // per set: 256 class totals + 256 cursors, cleared by the hist pass
+  scnt.ensure((size_t)nb * nsets * 4);
+  soff.ensure((size_t)nb * nsets * 4);
+  return g;
+}
+
+void BucketSort::scan(hipStream_t s, const Geom &g) {
+  size_t tb = g.scan_tmp;
+  MSM_HIP_CHECK(
+      hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, ghist.as<uint32_t>(), gbase.as<uint32_t>(), (int)g.nslots, s));
+}
+
+void BucketSort::run(hipStream_t s, const uint32_t *keys, const uint32_t *vals, size_t ne, uint32_t nb,
+                     uint32_t *sorted, uint32_t *counts, uint32_t *offsets, uint32_t *order, int nsets) {
+  const Geom g = prepare(s, ne, nb, nsets, 0);
+  hipLaunchKernelGGL(k_bs_hist, dim3(g.ntiles, nsets), dim3(256), 0, s, keys, ne, g.fb_bits, g.ncb, g.ntiles,
                      ghist.as<uint32_t>(), classes.as<uint32_t>());
   MSM_HIP_CHECK(hipGetLastError());
-  size_t tb = scan_tmp;
-  MSM_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, ghist.as<uint32_t>(), gbase.as<uint32_t>(), (int)nslots, s));
-  hipLaunchKernelGGL(k_bs_coarse, dim3(ntiles, nsets), dim3(256), (size_t)(2 * ncb + 2 * BS_TILE) * 4, s, keys, vals,
-                     ne, fb_bits, ncb, ntiles, gbase.as<uint32_t>(), okeys.as<uint32_t>(), ovals.as<uint32_t>());
+  scan(s, g);
+  hipLaunchKernelGGL(k_bs_coarse, dim3(g.ntiles, nsets), dim3(256), (size_t)(2 * g.ncb + 2 * BS_TILE) * 4, s, keys,
+                     vals, ne, g.fb_bits, g.ncb, g.ntiles, gbase.as<uint32_t>(), okeys.as<uint32_t>(),
+                     ovals.as<uint32_t>());
   MSM_HIP_CHECK(hipGetLastError());
+  finish(s, g, ne, nb, sorted, counts, offsets, order, nsets);
+}
+
+void BucketSort::finish(hipStream_t s, const Geom &g, size_t ne, uint32_t nb, uint32_t *sorted, uint32_t *counts,
+                        uint32_t *offsets, uint32_t *order, int nsets) {
+  (void)ne;
+  const int fb_bits = g.fb_bits, ncb = g.ncb, ntiles = g.ntiles;
+  const size_t nw = groups(nb);
   hipLaunchKernelGGL(k_bs_fine, dim3(ncb, nsets), dim3(1024), 0, s, okeys.as<uint32_t>(), ovals.as<uint32_t>(),
                      fb_bits, ncb, ntiles, gbase.as<uint32_t>(), ghist.as<uint32_t>(), nb, sorted, counts, offsets,
                      classes.as<uint32_t>(), nsets);
   MSM_HIP_CHECK(hipGetLastError());
-  scnt.ensure((size_t)nb * nsets * 4);
-  soff.ensure((size_t)nb * nsets * 4);
   hipLaunchKernelGGL(k_sched_scatter, dim3(nblk(nb, SCHED_PER_BLOCK), nsets), dim3(256), 0, s, counts, offsets, nb,
                      classes.as<uint32_t>(), order, scnt.as<uint32_t>(), soff.as<uint32_t>());
   MSM_HIP_CHECK(hipGetLastError());

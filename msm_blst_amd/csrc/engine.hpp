@@ -94,6 +94,19 @@ struct BucketSort {
   // shared `sorted` array of up to nsets ne entries), bucket_sort.hpp
   void run(hipStream_t s, const uint32_t *keys, const uint32_t *vals, size_t ne, uint32_t nb, uint32_t *sorted,
            uint32_t *counts, uint32_t *offsets, uint32_t *order, int nsets = 1);
+  // run() in pieces, for a caller that bins its entries itself (the fused CHES
+  // front, ches_kernels.hpp k_ches_front_hist / _coarse): prepare sizes every
+  // buffer for ntiles histogram tiles per set (0: ceil(ne / BS_TILE)); the
+  // caller fills ghist, scan() writes gbase, the caller bins into okeys / ovals,
+  // finish() runs the fine pass, the schedule and the interleave.
+  struct Geom {
+    int fb_bits = 8, ncb = 1, ntiles = 1;
+    size_t nslots = 0, scan_tmp = 0;
+  };
+  Geom prepare(hipStream_t s, size_t ne, uint32_t nb, int nsets, int ntiles);
+  void scan(hipStream_t s, const Geom &g);
+  void finish(hipStream_t s, const Geom &g, size_t ne, uint32_t nb, uint32_t *sorted, uint32_t *counts,
+              uint32_t *offsets, uint32_t *order, int nsets);
   size_t device_bytes() const {
     return ghist.bytes + gbase.bytes + okeys.bytes + ovals.bytes + classes.bytes + tmp.bytes + scnt.bytes + soff.bytes +
            wbase.bytes + ipay.bytes;
