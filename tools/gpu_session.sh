@@ -30,5 +30,7 @@ timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/cal_fetc
 timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/cal_write -o run -- $MB/gather_cal > $O/cal_write.log 2>&1 &&
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python3 $R/bench.py --steps 2 --warmup 0 --no-cpu-baseline --no-compare --no-batch > $O/pmc_fetch.log 2>&1 &&
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- python3 $R/bench.py --steps 2 --warmup 0 --no-cpu-baseline --no-compare --no-batch > $O/pmc_write.log 2>&1 &&
-echo "pmc ok $(date +%T)"
+echo "pmc ok $(date +%T)" &&
+python3 $R/tools/pmc_traffic.py $O/pmc_fetch/run_counter_collection.csv $O/pmc_write/run_counter_collection.csv ches 20 $O/pmc_traffic.json $R/profiles/r02_gather_cal.json > /dev/null &&
+grep accumulate_bytes_per_launch $O/pmc_traffic.json
 echo "rc=$?"
