@@ -115,7 +115,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--log-n", type=int, default=20, help="points per GPU = 2^log_n")
     ap.add_argument("--method", choices=("ches", "pippenger", "bgmw"), default="ches")
     ap.add_argument("--group", type=int, choices=(1, 2), default=1,
