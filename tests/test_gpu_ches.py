@@ -175,7 +175,8 @@ def test_mult_batch_sets_resident_and_pinned(m, group, log_n, K):
     the pipeline) equal the synchronous MSMs.  K = 9 and 17 also
     exceed one reduction group (kGroup = 8): several groups of uneven size R
     alternate between the two reducer buffer sets / tail streams and read back
-    at their own offsets, and the front groups (1, 1, 2, 4, 8, ...) straddle them."""
+    at their own offsets (test_batch_front_groups_of_eight repeats K = 17 / 9
+    with front groups of 1, 1, 2, 4, 8 straddling them)."""
     import numpy as np
     import torch
     n = 1 << log_n
@@ -234,3 +235,43 @@ def test_batch_front_groups_of_eight():
                        timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     assert "FRONT_GROUPS_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+_UNFUSED_SCRIPT = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+import msm_blst_amd as m
+out = []
+for group, log_n in ((1, 12), (2, 10)):
+    n = 1 << log_n
+    ctx = m.CHESContext(group, 0, n_exp=log_n)
+    ctx.build_table(m.fixed_points(group, n), n)
+    out.append(m.compress(group, ctx.mult(m.gen_scalars(n, 77))).hex())
+    ctx.close()
+print("RESULTS", " ".join(out))
+"""
+
+
+def test_unfused_front_equals_fused(m):
+    """The fused CHES front (ches_kernels.hpp k_ches_front_hist / _coarse: digits
+    counted per coarse bin, then recomputed and binned from registers; the default
+    for every h the reference configurations use except 15 and 22) and the unfused
+    one (k_ches_digits writing keys / vals, then BucketSort::run), selected with
+    MSM_FRONT_FUSED=0 in a child process (read once per process), give the same
+    MSMs for G1 2^12 (h = 19) and G2 2^10 (h = 20)."""
+    import os
+    import subprocess
+    import sys
+    want = []
+    for group, log_n in ((1, 12), (2, 10)):
+        n = 1 << log_n
+        ctx = m.CHESContext(group, 0, n_exp=log_n)
+        ctx.build_table(m.fixed_points(group, n), n)
+        want.append(m.compress(group, ctx.mult(m.gen_scalars(n, 77))).hex())
+        ctx.close()
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _UNFUSED_SCRIPT, repo], capture_output=True, text=True,
+                       env=dict(os.environ, MSM_FRONT_FUSED="0"), timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULTS")]
+    assert line and line[0].split()[1:] == want, r.stdout[-2000:]
