@@ -917,6 +917,19 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
   for (size_t g = 0; g < nsg; ++g) copy_group(g);
   // every group's copies are enqueued before its front (nsg >= kFronts - 1)
   static_assert(kFronts - 1 <= 2, "copy lead must cover the front lead");
+  // Accumulation k waits for level 0 of MSM k - 1, so level 0 runs beside the
+  // fronts, never beside the next accumulation.  Without this wait the batch
+  // fell, in about one run in three, into a schedule where fronts ran two MSMs
+  // ahead and every accumulation started at once beside the previous level 0:
+  // level 0 then took 0.5-1.2 ms instead of 0.41, the accumulations 2.2-2.7 ms
+  // instead of 1.8, and the H2D headline 342-386 M pairs/s instead of ~420
+  // (kernel traces, profiles/r03_spread_trace.txt); with it 19 of 19 runs on
+  // three boxes gave 410-422 M (profiles/r03_ab_studies.txt r03a0*).
+  // MSM_ACC_AFTER_L0=0 restores the free-running schedule.
+  static const bool l0_first = [] {
+    const char *e = getenv("MSM_ACC_AFTER_L0");
+    return !e || atoi(e) != 0;
+  }();
   for (size_t g = 0; g + 1 < (size_t)kFronts; ++g) front_group(g);
   for (size_t g = 0; g < nfg; ++g) {
     copy_group(g + nsg);
@@ -926,6 +939,7 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
       const int bset = (int)(k % kBSets), slot = (int)(k % R), gset = (int)((k / R) % 2);
       hipStream_t ts = tails_[gset];
       if (k >= (size_t)kBSets) MSM_HIP_CHECK(hipStreamWaitEvent(s, evh[k - kBSets], 0));  // bucket set free again
+      if (l0_first && k >= 1) MSM_HIP_CHECK(hipStreamWaitEvent(s, evh[k - 1], 0));
       if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k], s));
       accumulate(s, (int)(g % kFronts), (int)(k - fgb[g]), bset);
       if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k + 1], s));
