@@ -925,11 +925,14 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
   // instead of 1.8, and the H2D headline 342-386 M pairs/s instead of ~420
   // (kernel traces, profiles/r03_spread_trace.txt); with it 19 of 19 runs on
   // three boxes gave 410-422 M (profiles/r03_ab_studies.txt r03a0*).
-  // MSM_ACC_AFTER_L0=0 restores the free-running schedule.
-  static const bool l0_first = [] {
+  // G2 (5-ms accumulations, 1.2-ms level 0) never showed the slow mode and
+  // runs 1.5 % faster free-running (r03a0g2), so the wait is the G1 default;
+  // MSM_ACC_AFTER_L0=0 / =1 forces either schedule for both groups.
+  static const int l0_env = [] {
     const char *e = getenv("MSM_ACC_AFTER_L0");
-    return !e || atoi(e) != 0;
+    return e ? (atoi(e) != 0 ? 1 : 0) : -1;
   }();
+  const bool l0_first = l0_env < 0 ? G == 1 : l0_env == 1;
   for (size_t g = 0; g + 1 < (size_t)kFronts; ++g) front_group(g);
   for (size_t g = 0; g < nfg; ++g) {
     copy_group(g + nsg);
