@@ -1,31 +1,36 @@
 #!/usr/bin/env python3
-"""bench.py -- G1 MSM point-scalar pairs/s at n=2^20 per MI355X (BASELINE.json metric).
+"""bench.py -- G1 MSM point-scalar pairs/s at n=2^20 on 1/2/4/8 MI355X (BASELINE.json metric).
 
-One step = one complete G1 MSM over this rank's 2^20 fixed points by the
-reference's CHES "nh + q/5" method (BASELINE.json configs[2]: q = 2^22, h = 12,
-|B| = 874 437, precomputed table T = m q^j P_i resident in HBM), with its own
-scalar set: MB digit conversion -> bucket sort -> bucket accumulation ->
-weighted bucket reduction, plus, for N > 1, the single exchange of the partial
-sums (all_gather of 144-B Jacobians over RCCL) and their fold.
+One step = one complete G1 MSM of n = 2^20 point-scalar pairs by the
+reference's CHES "nh + q/5" method, split over the N ranks (strong scaling,
+the metric as stated: "pairs/sec at n=2^20, 1/2/4/8 MI355X"): rank r owns the
+contiguous points [r 2^20/N, (r+1) 2^20/N) and the CHES table of its shard,
+built with the reference's configuration for that shard size
+(ches_config_files/config_file_n_exp_{20 - log2 N}.h; at N = 1 configs[2]:
+q = 2^22, h = 12, |B| = 874 437, table T = m q^j P_i resident in HBM), and gets
+only its shard's scalars.  Per MSM: MB digit conversion -> bucket sort ->
+bucket accumulation -> weighted bucket reduction on every rank, then the single
+exchange of the partial sums (all_gather of 144-B Jacobians over RCCL) and
+their fold.
 
 Headline `value` ("scalars H2D included"): the K steps are K MSMs
 over K DISTINCT scalar sets that start in page-locked host memory; each set's
-32-MiB H2D copy is inside the timed region, issued by the pipelined batch
-(msm_ches_ctx_mult_batch) on its front stream so it overlaps earlier MSMs'
-accumulations.  Reported beside it: the same batch with the scalar sets already
-resident in HBM (`methods.ches_batch_resident`), K synchronous MSMs
-(`methods.ches_sync`), and the reference's other methods on the same points
-(plain Pippenger = configs[1] method, BGMW95).
+H2D copy is inside the timed region, issued by the pipelined batch
+(msm_ches_ctx_mult_batch) on its copy stream so it overlaps earlier MSMs'
+accumulations; one all_gather per batch.  value = 2^20 K / max-over-ranks time.
+Reported beside it: the same batch with the scalar sets already resident in
+HBM (`methods.ches_batch_resident`), K synchronous MSMs (`methods.ches_sync`),
+the reference's other methods on the same points (plain Pippenger = configs[1]
+method, BGMW95), and for N > 1 the weak-scaling leg (2^20 points per rank,
+`methods.ches_weak_2^20_per_rank`) and configs[3] (2^21 over the ranks).
 
 Parity (bit-exact): set 0 is the seed-1 scalar stream of BASELINE.md sec.3
-(rank r takes slice r of the N*2^20 stream), so the folded set-0 result is the
-golden MSM of N*2^20 points when tests/golden holds it; every batch result must
+(rank r takes its slice of the 2^20-scalar stream), so the folded set-0 result
+must equal the golden n = 2^20 MSM of tests/golden; every batch result must
 equal the synchronous MSM of the same set; the last set is recomputed by the
-reference's own multi-threaded CPU grid (cpu_baseline); for N > 1 without a
-golden value each rank's set-0 partial is cross-checked with plain Pippenger.
+reference's own multi-threaded CPU grid (cpu_baseline, N = 1).
 
-Weak scaling: every GPU owns its own 2^log_n-point shard of P_i = 2^(i+1) G.
-configs[3] (2^21 points over 8 GPUs): --log-n 18 --gpus 8.
+--log-n L instead fixes 2^L points per rank (weak scaling, the round-3 mode).
 
 Usage:
   python bench.py [--gpus N --steps K --warmup W]                 (N = 1)
@@ -48,8 +53,24 @@ MADS_PER_FPMUL = 392           # 14x14 product + 14x14 reduction, one v_mad_u64_
 FPMUL_PEAK = 76.8e9            # measured register-resident Fp-mul/s: profiles/r02_fp_rate.txt (tools/microbench/fp_rate.hip)
 AFFINE_BYTES = 96              # one G1 affine point (blst layout), SURVEY 8d
 FPMUL_PER_MADD = 10            # 8M + 2S (ec_ops.h:727-748)
+MAD_RATE = 30.36e12            # measured chip v_mad_u64_u32 issue rate (lane-ops/s): profiles/r02_instr_rate.txt
 CPU_THREADS = 16               # the GPU box's CPU share per GPU (16 threads)
 DEFAULT_BETA = {}              # log_n -> ches_config_files variant used by default; _beta at 2^20 measured slower
+
+
+def isa_mads_per_madd(path=os.path.join(REPO, "profiles", "r04_isa_counts.txt")):
+    """v_mad_u64_u32 per G1 xyzz madd on its main path, from the gfx950 ISA of
+    the shipped field code (tools/isa_report.sh): the madd is 6 products
+    (U2, S2, PPP, Q, ZZ3, ZZZ3), 2 squares (PP, R^2) and one fused two-product
+    sum (Y3 = R (Q - X3) - S1 PPP), ec.hpp xyzz_madd."""
+    import re
+    try:
+        txt = open(path).read()
+        cnt = {k: int(re.search(k + r"\w*\n\s+vgpr \d+ scratch \d+ total \d+ v_mad_u64_u32 (\d+)", txt).group(1))
+               for k in ("k_op_fp_mulP", "k_op_fp_sqr", "k_op_fp_mul2")}
+        return 6 * cnt["k_op_fp_mulP"] + 2 * cnt["k_op_fp_sqr"] + cnt["k_op_fp_mul2"], os.path.basename(path)
+    except Exception:
+        return 3567, "profiles/r03_isa_counts.txt (constant)"
 
 
 def log(*a):
@@ -116,7 +137,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--log-n", type=int, default=20, help="points per GPU = 2^log_n")
+    ap.add_argument("--log-n", type=int, default=None,
+                    help="weak scaling: 2^log_n points per GPU (default: strong scaling, 2^log_n_total / N per GPU)")
+    ap.add_argument("--log-n-total", type=int, default=20, help="strong scaling: total points 2^log_n_total")
+    ap.add_argument("--no-weak-leg", action="store_true", help="N > 1: skip the 2^20-points-per-rank leg")
     ap.add_argument("--method", choices=("ches", "pippenger", "bgmw"), default="ches")
     ap.add_argument("--group", type=int, choices=(1, 2), default=1,
                     help="1: G1 (the BASELINE metric); 2: G2 (configs[4], Fp2 tower), reported under its own metric")
@@ -147,6 +171,13 @@ def main():
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
 
+    if args.log_n is None:  # strong scaling: one 2^log_n_total MSM split over the ranks
+        if world & (world - 1) or world > (1 << args.log_n_total):
+            raise SystemExit(f"strong scaling needs a power-of-two world size <= 2^{args.log_n_total}, got {world}")
+        args.log_n = args.log_n_total - (world.bit_length() - 1)
+        scaling = "strong"
+    else:
+        scaling = "weak"
     import torch
     if args.one_device:
         local = 0
@@ -318,6 +349,8 @@ def main():
     # shards of one process (--multi-context), against the golden 2^21 result
     if G == 1 and not args.no_compare and world > 1 and (1 << 21) % world == 0:
         others.update(cfg3_ranks(m, mdist, torch, dev, local, sp, world, rank, K, W, xdev, add))
+    if G == 1 and not args.no_compare and world > 1 and scaling == "strong" and not args.no_weak_leg:
+        others.update(weak_leg(m, mdist, torch, dev, local, sp, world, rank, K, W, xdev, add))
     if G == 1 and world == 1 and args.multi_context > 1:
         others.update(cfg3_multi_context(m, torch, args.multi_context, args.one_device, K, W))
 
@@ -368,6 +401,7 @@ def main():
             traffic = None
     fpm_per_madd = FPMUL_PER_MADD if G == 1 else 28   # Fp2: 8M + 2S = 8*3 + 2*2 Fp-mul
     fpmul_rate = madds * fpm_per_madd / acc_s
+    mads, mads_src = isa_mads_per_madd()
 
     parity = golden_ok if golden_ok is not None else cross
     if batch_eq_sync is False:
@@ -381,13 +415,15 @@ def main():
         "warmup": W,
         "ms_per_step": round(elapsed / K * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "u32 (exact Fp381 integer arithmetic, 14x28-bit limbs)" + ("" if G == 1 else ", Fp2 = Fp[i]/(i^2+1)"),
         "data": ("synthetic: P_i = 2^(i+1) G%d (main_p1.cpp:52-66), SplitMix64 scalars < r (BASELINE.md sec.3), "
                  "K distinct scalar sets" % G),
         "config": dict({"workload": workload, "n_per_gpu": n, "n_total": n * world,
-                        "parallelism": f"points sharded x{world}, RCCL all_gather of {144 * G}-B partials"}, **cfg_extra),
+                        "parallelism": (f"one n=2^{args.log_n + world.bit_length() - 1} MSM: points sharded x{world}, "
+                                        f"RCCL all_gather of {144 * G}-B partials" if world > 1 else "1 GPU")},
+                       **cfg_extra),
         "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved_gbs / HBM_PEAK_GBS, 5), "traffic": traffic,
                      "kernel": "k_accumulate (bucket accumulation)", "kernel_ms": round(acc_s * 1e3, 4),
@@ -402,7 +438,15 @@ def main():
                           "frac_alone": (round(madds * fpm_per_madd / (phases["accumulate"] / 1e3) / FPMUL_PEAK, 4)
                                          if phases.get("accumulate") else None),
                           "alone_basis": "the same kernel in one synchronous MSM (phases_ms.accumulate): no front or "
-                                         "reduction of a neighbouring MSM shares its SIMDs"},
+                                         "reduction of a neighbouring MSM shares its SIMDs",
+                          # hardware-anchored: v_mad_u64_u32 issued per launch vs the measured chip mad rate
+                          "mad_frac": round(madds * mads / acc_s / MAD_RATE, 4) if G == 1 else None,
+                          "mad_frac_alone": (round(madds * mads / (phases["accumulate"] / 1e3) / MAD_RATE, 4)
+                                             if G == 1 and phases.get("accumulate") else None),
+                          "mads_per_madd": mads if G == 1 else None, "mad_rate_peak": MAD_RATE,
+                          "mad_basis": (f"{madds} madds x {mads} v_mad_u64_u32 (6 mul + 2 sqr + 1 two-product sum, "
+                                        f"gfx950 ISA counts {mads_src}) / kernel time / {MAD_RATE / 1e12:.2f} T "
+                                        f"mad/s (profiles/r02_instr_rate.txt)")},
         "phases_ms": {k: round(v, 4) for k, v in phases.items()},
         "phases_note": "one synchronous MSM (profiled) after the timed region" if batched else "last timed step",
         "pipelined_batch": batched,
@@ -596,6 +640,38 @@ def _cfg3_sets(m, K, lo, hi):
         full = np.frombuffer(m.gen_scalars(N, 1 if k == 0 else 5000 + k), dtype=np.uint8)
         host.numpy()[k * n * 32:(k + 1) * n * 32] = full[lo * 32:hi * 32]
     return host
+
+
+def weak_leg(m, mdist, torch, dev, local, sp, world, rank, K, W, xdev, add):
+    """The round-3 weak-scaling mode as a leg: every rank owns its own 2^20
+    points (configs[2] per rank, n_total = N 2^20), K distinct host scalar sets
+    per rank (set 0 = slice `rank` of the seed-1 stream of N 2^20 scalars),
+    pipelined batch with H2D, one all_gather of the batch's partials.  Parity:
+    the folded set 0 against the golden N 2^20 MSM where tests/golden holds it
+    (N = 2: 2^21), and on every rank the batch against the synchronous MSM."""
+    n = 1 << 20
+    start, _ = mdist.shard_range(n * world, world, rank)
+    t = time.time()
+    ctx = m.CHESContext(1, local, n_exp=20)
+    ctx.build_table(m.fixed_points(1, n, start), n, stream=sp)
+    host = make_scalar_sets(m, n, K, rank, world)
+    torch.cuda.synchronize(dev)
+    setup = time.time() - t
+    ctx.mult_batch(host.data_ptr(), min(max(W, 1), K), 32, set_stride=n * 32, on_device=False, stream=sp)
+    with Bracket(world, dev, xdev) as b:
+        parts = ctx.mult_batch(host.data_ptr(), K, 32, set_stride=n * 32, on_device=False, stream=sp)
+        res = [mdist.fold(ps, add) for ps in mdist.gather_partials_batch(parts, 1, xdev)]
+    sync0 = ctx.mult(host.data_ptr(), 32, on_device=False, stream=sp)
+    eq = all_true(m.compress(1, sync0) == m.compress(1, parts[0]), world, xdev)
+    want = _golden(m, 1, n * world)
+    ok = all_true(m.compress(1, res[0]).hex() == want, world, xdev) if want else None
+    ctx.close()
+    return {"ches_weak_2^20_per_rank": {
+        "value": round(n * world * K / b.elapsed, 1), "unit": "pairs/s", "ms_per_step": round(b.elapsed / K * 1e3, 4),
+        "n_total": n * world, "parity_vs_reference": ok, "batch_equals_sync_set0_all_ranks": eq,
+        "setup_s": round(setup, 2), "scaling": "weak",
+        "note": f"weak scaling: {world} ranks x 2^20 points (config_file_n_exp_20.h per rank), {K} distinct scalar "
+                f"sets H2D from pinned memory, one all_gather of the batch's partials"}}
 
 
 def cfg3_ranks(m, mdist, torch, dev, local, sp, world, rank, K, W, xdev, add):

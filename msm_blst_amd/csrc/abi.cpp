@@ -650,9 +650,9 @@ void msm_engine_cache_stats(size_t out[3]) {
 }
 
 size_t msm_set_engine_cache_limit(size_t bytes) {
-  std::lock_guard<std::mutex> g(PoolRegistry::get().mu);
-  const size_t prev = PoolRegistry::get().idle_budget;
-  PoolRegistry::get().idle_budget = bytes;
+  const size_t prev = PoolRegistry::get().idle_budget.exchange(bytes);
+  PoolStats st;  // a lowered limit trims the engines already idle
+  PoolRegistry::get().visit(st, false);
   return prev;
 }
 

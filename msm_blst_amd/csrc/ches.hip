@@ -549,6 +549,21 @@ void Ches<G>::plan_buckets(size_t n) {
   red_.plan(w);
 }
 
+// Accumulation lanes of a batch (run_batch): 2 when one accumulation's lanes
+// (one per bucket for G1, two for G2) fill fewer than ~3 rounds of the chip's
+// wave slots (1024 SIMDs x 3 waves x 64 lanes), else 1.  MSM_BATCH_LANES=1|2|3
+// overrides.
+template <int G>
+int Ches<G>::batch_lanes() const {
+  static const int env = [] {
+    const char *e = getenv("MSM_BATCH_LANES");
+    return e ? std::max(1, std::min(3, atoi(e))) : 0;
+  }();
+  if (env) return env;
+  const size_t lanes = bucket_count() * (G == 2 ? 2 : 1);
+  return lanes < (size_t)3 * 3 * 1024 * 64 ? 2 : 1;
+}
+
 template <int G>
 void Ches<G>::build_table(const void *pts, size_t n, bool on_device, hipStream_t s) {
   typedef typename FieldOf<G>::F F;
@@ -815,7 +830,8 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
   // every buffer the loop touches exists before the first launch (an allocation
   // inside the issue loop could synchronise the device)
   const size_t NB = bucket_count(), n = n_;
-  for (int b = 0; b < kBSets; ++b) buckets_[b].ensure(NB * sizeof(Xyzz<typename FieldOf<G>::F>));
+  const int nl = batch_lanes();
+  for (int b = 0; b < std::max(kBSets, nl); ++b) buckets_[b].ensure(NB * sizeof(Xyzz<typename FieldOf<G>::F>));
   // sized for kGroup whatever this batch's R: a later, larger batch must not
   // reallocate (a hipFree inside the pipelined region would synchronise it)
   // (both reducer sets, and both bucket sets, whatever this batch's length: a
@@ -874,12 +890,12 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
   // Reducer set t is reused by group q + 2 only after group q's tail: both are
   // in order on tails_[t].
   // dependency events for at least 64 MSMs, created once (not inside a timed batch)
-  while (bev_.size() < std::max<size_t>(3 * count + 2 * nfg + 1, 3 * 64 + 2 * 64 + 1)) {
+  while (bev_.size() < std::max<size_t>(3 * count + 2 * nfg + ngroups + 1, 3 * 64 + 3 * 64 + 1)) {
     hipEvent_t e;
     MSM_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     bev_.push_back(e);
   }
-  hipEvent_t *eva = bev_.data() + 1, *evh = eva + count, *evf = evh + count, *evc = evf + nfg;
+  hipEvent_t *eva = bev_.data() + 1, *evh = eva + count, *evf = evh + count, *evc = evf + nfg, *evt = evc + nfg;
   MSM_HIP_CHECK(hipEventRecord(bev_[0], s));  // the batch starts after prior work on s
   MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, bev_[0], 0));
   MSM_HIP_CHECK(hipStreamWaitEvent(cstream_, bev_[0], 0));
@@ -909,7 +925,12 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
     if (g >= nfg) return;
     const bool copied = scalars_on_host && !zero_copy;
     if (copied) MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, evc[g], 0));
-    if (g >= (size_t)kFronts) MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, eva[fgb[g - kFronts + 1] - 1], 0));
+    if (g >= (size_t)kFronts) {  // front set g % kFronts: every accumulation of group g - kFronts has read it
+      const size_t last = fgb[g - kFronts + 1] - 1;
+      MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, eva[last], 0));
+      for (size_t d = 1; d < (size_t)nl && last >= d && last - d >= fgb[g - kFronts]; ++d)  // its other lanes
+        MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, eva[last - d], 0));
+    }
     const uint8_t *src = copied ? slots(g) : scalars + fgb[g] * set_stride;
     digits_sort(fstream_, src, stride, copied ? sslot : set_stride, (int)(fgb[g + 1] - fgb[g]), (int)(g % kFronts));
     MSM_HIP_CHECK(hipEventRecord(evf[g], fstream_));
@@ -934,7 +955,44 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
   }();
   const bool l0_first = l0_env < 0 ? G == 1 : l0_env == 1;
   for (size_t g = 0; g + 1 < (size_t)kFronts; ++g) front_group(g);
-  for (size_t g = 0; g < nfg; ++g) {
+  // Two accumulation lanes (small MSMs, batch_lanes()): MSM k accumulates into
+  // bucket set k % 2 on lane stream k % 2 (the caller's s, tails_[0]) and its
+  // level 0 follows on the same stream, so accumulations k and k + 1 run side
+  // by side -- one small accumulation (a few hundred thousand buckets, one lane
+  // each) fills the chip's 3 x 1024 wave slots only ~1 round deep, and its last
+  // waves run alone -- while the group tails run on tails_[1].  Bucket set k % 2
+  // is reused by lane k % 2 only, in stream order; reducer set q % 2 is reused
+  // by group q + 2 after tail q (event evt[q]).
+  // Three lanes (MSM_BATCH_LANES=3) add tails_[1] as a lane and move the group
+  // tails to the front stream (the process has 4 hardware queues by default,
+  // GPU_MAX_HW_QUEUES: one stream per queue).
+  if (nl >= 2) {
+    hipStream_t lane[3] = {s, tails_[0], tails_[1]}, ts = nl == 3 ? fstream_ : tails_[1];
+    for (size_t g = 0; g < nfg; ++g) {
+      copy_group(g + nsg);
+      front_group(g + kFronts - 1);
+      for (size_t k = fgb[g]; k < fgb[g + 1]; ++k) {
+        hipStream_t L = lane[k % nl];
+        const int bset = (int)(k % nl), slot = (int)(k % R), gset = (int)((k / R) % 2);
+        const size_t q = k / R;
+        MSM_HIP_CHECK(hipStreamWaitEvent(L, evf[g], 0));
+        if (q >= 2 && slot < nl) MSM_HIP_CHECK(hipStreamWaitEvent(L, evt[q - 2], 0));  // reducer set q % 2 free
+        if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k], L));
+        accumulate(L, (int)(g % kFronts), (int)(k - fgb[g]), bset);
+        if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k + 1], L));
+        MSM_HIP_CHECK(hipEventRecord(eva[k], L));
+        red_.launch_head_slot(L, buckets_[bset].p, gset, slot);
+        MSM_HIP_CHECK(hipEventRecord(evh[k], L));
+        if ((size_t)slot + 1 == R || k + 1 == count) {  // the group's level 0s are done on both lanes
+          for (int d = 0; d < nl && d <= slot; ++d) MSM_HIP_CHECK(hipStreamWaitEvent(ts, evh[k - d], 0));
+          red_.launch_tail_group(ts, gset, slot + 1);
+          red_.copy_out_group(ts, gset, slot + 1, (uint8_t *)host_out_ + (k - slot) * ob);
+          MSM_HIP_CHECK(hipEventRecord(evt[q], ts));
+        }
+      }
+    }
+  }
+  for (size_t g = 0; g < (nl >= 2 ? 0 : nfg); ++g) {
     copy_group(g + nsg);
     front_group(g + kFronts - 1);  // may start as soon as group g - 1's accumulations release its front set
     MSM_HIP_CHECK(hipStreamWaitEvent(s, evf[g], 0));
@@ -964,6 +1022,7 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
     MSM_HIP_CHECK(hipStreamWaitEvent(s, ev_tail_[t], 0));
   }
   for (int t = 0; t < kBSets; ++t) MSM_HIP_CHECK(hipStreamSynchronize(tails_[t]));
+  MSM_HIP_CHECK(hipStreamSynchronize(fstream_));  // three lanes: the group read-backs ran on the front stream
   for (size_t k = 0; k < count; ++k) outs[k] = red_.combine((const uint8_t *)host_out_ + k * ob)[0];
   profile_ = prof;
   if (prof) {  // average accumulation time over the batch (HIP events on stream s)

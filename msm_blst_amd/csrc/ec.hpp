@@ -63,6 +63,27 @@ MSM_FN void xyzz_dbl(Xyzz<F> &r, const Xyzz<F> &a) {
     r = a;
     return;
   }
+#if MSM_DBL_LEAN
+  // (study build, tools/r04_g2table.sh) ordered so that each input coordinate
+  // dies at its last use: ZZ3, ZZZ3 first
+  F U, V, W, S, M, t, X3;
+  f_add(U, a.y, a.y);      // < 4p lazy
+  f_sqr(V, U);             // S
+  f_mul(W, V, U);          // S
+  f_mul(S, a.x, V);        // S
+  f_mul(r.zz, V, a.zz);    // ZZ3 = V ZZ (V, ZZ die)
+  f_mul(r.zzz, W, a.zzz);  // ZZZ3 = W ZZZ
+  f_sqr(M, a.x);           // S (X dies)
+  f_mul3(M, M);            // < 6p lazy
+  f_sqr(X3, M);            // S
+  F z;
+  f_zero(z);
+  f_sub_2x(X3, X3, z, S);  // M^2 + 8p - 2S   < 10p
+  f_norm(X3);              // X
+  f_sub16(t, S, X3);       // < 18p
+  f_mul_sub(r.y, t, M, W, a.y);  // Y3 = M (S - X3) - W Y   S (one reduction)
+  r.x = X3;
+#else
   F U, V, W, S, M, t, X3, Y3;
   f_add(U, a.y, a.y);      // < 4p lazy
   f_sqr(V, U);             // S
@@ -81,6 +102,7 @@ MSM_FN void xyzz_dbl(Xyzz<F> &r, const Xyzz<F> &a) {
   f_mul(r.zzz, W, a.zzz);
   r.y = Y3;
   r.x = X3;
+#endif
 }
 
 // acc += (neg ? -P : P); P affine, canonical, not infinity (callers skip the

@@ -108,6 +108,14 @@ Pippenger<G>::~Pippenger() {
 }
 
 template <int G>
+size_t Pippenger<G>::device_bytes() const {
+  size_t b = stage_ ? stage_->pinned_bytes() : 0;
+  for (const DevBuf *d : {&pts_, &keys_, &vals_, &counts_, &offsets_, &sorted_, &order_, &buckets_, &tmp_, &scal_})
+    b += d->bytes;
+  return b + sort_.device_bytes();
+}
+
+template <int G>
 void Pippenger<G>::set_points(const void *pts, size_t n, bool on_device, hipStream_t s) {
   typedef typename FieldOf<G>::F F;
   DeviceGuard g(dev_);
@@ -260,6 +268,11 @@ void Pippenger<G>::run_host(hipStream_t s, const void *pts_blst, size_t n, const
     MSM_HIP_CHECK(hipEventCreateWithFlags(&ev_s_, hipEventDisableTiming));
   }
   if (!stage_) stage_ = std::make_unique<HostStager>();
+  // the point upload (stream up_) must not overwrite points an earlier MSM on s
+  // still reads; recorded before this call's front so the upload overlaps the
+  // scalars' digits and sort instead of queueing behind them
+  MSM_HIP_CHECK(hipEventRecord(ev_s_, s));
+  MSM_HIP_CHECK(hipStreamWaitEvent(up_, ev_s_, 0));
   const size_t sbytes = n * stride;
   scal_.ensure(sbytes + (tile ? n * 5 : 0) + 16);
   stage_->upload(scal_.p, scalars, sbytes, s);
@@ -274,9 +287,6 @@ void Pippenger<G>::run_host(hipStream_t s, const void *pts_blst, size_t n, const
   } else {
     front(s, scal_.as<uint8_t>(), stride, nbits, nullptr);
   }
-  // the upload stream must not overwrite points an earlier MSM on s still reads
-  MSM_HIP_CHECK(hipEventRecord(ev_s_, s));
-  MSM_HIP_CHECK(hipStreamWaitEvent(up_, ev_s_, 0));
   const size_t raw = n * 96 * G;
   tmp_.ensure(raw);
   pts_.ensure(n * sizeof(Aff<F>));

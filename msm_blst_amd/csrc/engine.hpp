@@ -261,12 +261,9 @@ class Pippenger {
   const PhaseTimes &times() const { return times_; }
   int device() const { return dev_; }
   int window_bits() const { return c_; }
-  size_t device_bytes() const {
-    size_t b = 0;
-    for (const DevBuf *d : {&pts_, &keys_, &vals_, &counts_, &offsets_, &sorted_, &order_, &buckets_, &tmp_, &scal_})
-      b += d->bytes;
-    return b;
-  }
+  // bytes this engine holds: device buffers plus its pinned upload ring (the
+  // engine pool's idle budget and cache stats count both, pool.hpp)
+  size_t device_bytes() const;
 
  private:
   int dev_, c_;
@@ -345,12 +342,14 @@ class Ches {
   // digit goes to copy i % copies_ of its bucket (copies share the weight B[k])
   int small_ = 0, copies_ = 1;
   void plan_buckets(size_t n);
+  int batch_lanes() const;  // accumulation streams of run_batch (1 or 2)
   bool profile_ = false;
   PhaseTimes times_;
   // bucket sets: MSM k accumulates into set k % kBSets while the reduction of
   // MSM k-1 still reads the other one
   static constexpr int kBSets = 2;
-  DevBuf code_, rank_, table_, buckets_[kBSets];
+  static constexpr int kLanesMax = 3;  // batch accumulation lanes (batch_lanes), one bucket set each
+  DevBuf code_, rank_, table_, buckets_[kLanesMax];
   // digit/sort outputs.  A batch can run the fronts (digits + sort) of up to
   // kFrontGroup MSMs in ONE pass per stage (seven launches for the group instead
   // of seven per MSM), front group g+2 beside group g's accumulations, three

@@ -144,42 +144,46 @@ inline bool host_pinned(const void *p) {
 }
 
 // Pinned ring for host -> device uploads; one per engine (engines are leased by
-// one thread at a time, pool.hpp).
+// one thread at a time, pool.hpp).  The ring is sized for the uploads it has
+// seen -- kSlots slots of min(kChunk, bytes / kSlots rounded up to 1 MiB) --
+// and grows (after its pending DMAs finish) only when a larger upload arrives,
+// so an engine serving small calls (a Go tile, a 2^12-point MSM) holds a few
+// MiB of page-locked memory, not 64.  Uploads below kDirect bytes skip the ring
+// (HIP's own staged pageable copy).
 class HostStager {
  public:
   static constexpr size_t kChunk = (size_t)16 << 20;
+  static constexpr size_t kMinSlot = (size_t)1 << 20;
+  static constexpr size_t kDirect = (size_t)1 << 20;
   static constexpr int kSlots = 4;
   HostStager() = default;
   HostStager(const HostStager &) = delete;
   HostStager &operator=(const HostStager &) = delete;
-  ~HostStager() {
-    for (int k = 0; k < kSlots; ++k)
-      if (ev_[k]) {
-        (void)hipEventSynchronize(ev_[k]);
-        (void)hipEventDestroy(ev_[k]);
-      }
-    if (ring_) (void)hipHostFree(ring_);
-  }
-  size_t pinned_bytes() const { return ring_ ? kChunk * kSlots : 0; }
+  ~HostStager() { release(); }
+  size_t pinned_bytes() const { return ring_ ? slot_ * kSlots : 0; }
 
   // dst (device) <- src (host), enqueued on s; returns when every chunk is
   // enqueued and src is no longer read.  Pinned sources go straight to the DMA.
   void upload(void *dst, const void *src, size_t bytes, hipStream_t s) {
     if (!bytes) return;
-    if (host_pinned(src)) {
+    if (bytes < kDirect || host_pinned(src)) {
       MSM_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
       return;
     }
-    if (!ring_) {
-      MSM_HIP_CHECK(hipHostMalloc(&ring_, kChunk * kSlots, hipHostMallocDefault));
+    const size_t want = std::min(kChunk, std::max(kMinSlot, ((bytes + kSlots - 1) / kSlots + kMinSlot - 1) &
+                                                                ~(kMinSlot - 1)));
+    if (!ring_ || want > slot_) {
+      release();
+      MSM_HIP_CHECK(hipHostMalloc(&ring_, want * kSlots, hipHostMallocDefault));
+      slot_ = want;
       for (int k = 0; k < kSlots; ++k) MSM_HIP_CHECK(hipEventCreateWithFlags(&ev_[k], hipEventDisableTiming));
     }
-    for (size_t off = 0; off < bytes; off += kChunk) {
+    for (size_t off = 0; off < bytes; off += slot_) {
       const int k = next_;
       next_ = (next_ + 1) % kSlots;
       if (used_[k]) MSM_HIP_CHECK(hipEventSynchronize(ev_[k]));  // the slot's previous DMA is done
-      const size_t len = std::min(kChunk, bytes - off);
-      uint8_t *slot = static_cast<uint8_t *>(ring_) + (size_t)k * kChunk;
+      const size_t len = std::min(slot_, bytes - off);
+      uint8_t *slot = static_cast<uint8_t *>(ring_) + (size_t)k * slot_;
       parallel_memcpy(slot, static_cast<const uint8_t *>(src) + off, len);
       MSM_HIP_CHECK(hipMemcpyAsync(static_cast<uint8_t *>(dst) + off, slot, len, hipMemcpyHostToDevice, s));
       MSM_HIP_CHECK(hipEventRecord(ev_[k], s));
@@ -189,9 +193,24 @@ class HostStager {
 
  private:
   void *ring_ = nullptr;
+  size_t slot_ = 0;
   hipEvent_t ev_[kSlots] = {};
   bool used_[kSlots] = {};
   int next_ = 0;
+  void release() noexcept {  // waits for the ring's pending DMAs
+    for (int k = 0; k < kSlots; ++k) {
+      if (ev_[k]) {
+        if (used_[k]) (void)hipEventSynchronize(ev_[k]);
+        (void)hipEventDestroy(ev_[k]);
+      }
+      ev_[k] = nullptr;
+      used_[k] = false;
+    }
+    if (ring_) (void)hipHostFree(ring_);
+    ring_ = nullptr;
+    slot_ = 0;
+    next_ = 0;
+  }
 };
 
 }  // namespace msm

@@ -14,6 +14,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <exception>
 #include <functional>
 #include <map>
 #include <memory>
@@ -33,11 +35,13 @@ struct PoolStats {
 struct PoolRegistry {
   std::mutex mu;
   std::vector<std::function<void(PoolStats &, bool release)>> pools;
-  size_t idle_budget = (size_t)8 << 30;  // bytes of idle engines kept per device and pool
+  std::atomic<size_t> idle_budget{(size_t)8 << 30};  // bytes of idle engines kept per device and pool
   static PoolRegistry &get() {
     static PoolRegistry *r = new PoolRegistry();  // never destroyed: engines may outlive static teardown
     return *r;
   }
+  // release: free every idle engine; otherwise (stats) idle engines beyond a
+  // lowered idle_budget are trimmed
   void visit(PoolStats &st, bool release) {
     std::vector<std::function<void(PoolStats &, bool)>> copy;
     {
@@ -60,10 +64,18 @@ class EnginePool {
   };
   class Lease {
    public:
-    Lease(EnginePool *p, Key k, Slot sl) : p_(p), k_(k), sl_(std::move(sl)) {}
+    Lease(EnginePool *p, Key k, Slot sl) : p_(p), k_(k), sl_(std::move(sl)), exc_(std::uncaught_exceptions()) {}
     Lease(const Lease &) = delete;
     Lease &operator=(const Lease &) = delete;
-    ~Lease() { p_->put(k_, std::move(sl_)); }
+    // A call that throws (a HIP error, bad arguments) may leave copies reading
+    // the caller's buffers or kernels queued on the engine's stream, and the
+    // engine in an unknown state: during unwinding (or after poison()) the
+    // stream is drained and the engine destroyed instead of returned to the pool.
+    ~Lease() {
+      if (poisoned_ || std::uncaught_exceptions() > exc_) p_->discard(std::move(sl_));
+      else p_->put(k_, std::move(sl_));
+    }
+    void poison() { poisoned_ = true; }
     E &operator*() { return *sl_.e; }
     E *operator->() { return sl_.e.get(); }
     hipStream_t stream() const { return sl_.s; }
@@ -72,6 +84,8 @@ class EnginePool {
     EnginePool *p_;
     Key k_;
     Slot sl_;
+    int exc_;
+    bool poisoned_ = false;
   };
 
   static EnginePool &get() {
@@ -138,10 +152,18 @@ class EnginePool {
     if (!sl.e) return;
     {
       std::lock_guard<std::mutex> g(mu_);
-      if (idle_bytes_dev(k.first) + sl.e->device_bytes() <= PoolRegistry::get().idle_budget) {
+      if (idle_bytes_dev(k.first) + sl.e->device_bytes() <= PoolRegistry::get().idle_budget.load()) {
         idle_[k].push_back(std::move(sl));
         return;
       }
+      --live_;
+    }
+    destroy(sl);
+  }
+  void discard(Slot sl) noexcept {  // never cached (~Lease during unwinding)
+    if (!sl.e) return;
+    {
+      std::lock_guard<std::mutex> g(mu_);
       --live_;
     }
     destroy(sl);
@@ -154,6 +176,24 @@ class EnginePool {
         for (auto &kv : idle_)
           for (auto &sl : kv.second) drop.push_back(std::move(sl));
         idle_.clear();
+        live_ -= drop.size();
+      } else {  // trim each device's idle engines to the (possibly lowered) budget
+        const size_t budget = PoolRegistry::get().idle_budget.load();
+        std::map<int, size_t> held;
+        for (auto &kv : idle_) {
+          auto &v = kv.second;
+          for (size_t i = 0; i < v.size();) {
+            size_t &h = held[kv.first.first];
+            const size_t b = v[i].e->device_bytes();
+            if (h + b <= budget) {
+              h += b;
+              ++i;
+            } else {
+              drop.push_back(std::move(v[i]));
+              v.erase(v.begin() + (long)i);
+            }
+          }
+        }
         live_ -= drop.size();
       }
       st.live += live_;

@@ -88,3 +88,49 @@ def test_concurrent_calls_are_bounded_and_released(m, golden, points):
     _call(m, pts, sc, out)
     assert out == [_golden(golden)]
     assert m.engine_cache_stats() == (0, 0, 0)
+
+
+def test_lowered_limit_trims_idle_engines(m, golden, points):
+    """msm_set_engine_cache_limit trims engines that are already idle (the
+    limit is read atomically by every returning call, csrc/pool.hpp)."""
+    pts, sc = points(1, N), m.gen_scalars(N, 1)
+    out = []
+    _call(m, pts, sc, out)
+    assert m.engine_cache_stats()[:2] == (1, 1)
+    m.set_engine_cache_limit(0)
+    assert m.engine_cache_stats() == (0, 0, 0)
+    assert out == [_golden(golden)]
+
+
+def test_small_calls_hold_no_large_pinned_ring(m, points):
+    """A 2^12-point call uploads < 1 MiB per buffer: no pinned ring is
+    allocated, so the cached engine holds only its device buffers (the ring was
+    a fixed 64 MiB per engine, counted nowhere)."""
+    pts, sc = points(1, N), m.gen_scalars(N, 1)
+    _call(m, pts, sc, [])
+    _, idle, idle_bytes = m.engine_cache_stats()
+    assert idle == 1 and 0 < idle_bytes < (64 << 20)
+
+
+def test_failed_call_drops_its_engine(m, golden, points):
+    """A call that throws after leasing its engine (nbits > 256 is rejected on
+    the device path) must not return the engine to the pool: it is drained and
+    destroyed during unwinding.  The next call gets a fresh engine and the
+    golden result."""
+    pts, sc = points(1, N), m.gen_scalars(N, 1)
+    L = m.lib()
+    prev = L.msm_set_abort_on_error(0)
+    try:
+        wide = (ctypes.c_uint8 * (N * 40))()
+        pp = (ctypes.c_void_p * 2)(ctypes.cast(pts, ctypes.c_void_p), None)
+        sp = (ctypes.c_void_p * 2)(ctypes.cast(wide, ctypes.c_void_p), None)
+        r = (ctypes.c_uint8 * 144)()
+        L.blst_p1s_mult_pippenger(r, pp, N, sp, 300, None)
+        assert L.msm_error_pending()
+        L.msm_last_error()
+        assert m.engine_cache_stats() == (0, 0, 0)
+    finally:
+        L.msm_set_abort_on_error(prev)
+    out = []
+    _call(m, pts, sc, out)
+    assert out == [_golden(golden)]
