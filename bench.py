@@ -263,6 +263,10 @@ def main():
     batched = args.method == "ches" and not args.no_batch
     legs = {}
     if batched:
+        pre = float(os.environ.get("BENCH_PREHEAT_MS", "0"))  # study knob: untimed sync MSMs before the warmup
+        t_pre = time.perf_counter()
+        while (time.perf_counter() - t_pre) * 1e3 < pre:
+            mult(0)
         if W:
             ctx.mult_batch(hptr, min(W, K), 32, set_stride=SS, on_device=False, stream=sp)
         with Bracket(world, dev, xdev) as b:  # headline: host scalars, H2D inside the pipeline
@@ -520,7 +524,22 @@ def config_legs(m, torch, dev, local, sp, pts, host, K, W):
             "value": round(n16 * K / el, 1), "unit": "pairs/s", "ms_per_step": round(el / K * 1e3, 4),
             "phases_ms": {kk: round(v, 4) for kk, v in pc.phase_times().items()},
             "parity_vs_reference": m.compress(1, r[0]).hex() == want16,
-            "note": f"configs[1]: msm_ctx_mult, window c={c}, points and {K} scalar sets resident in HBM"}
+            "note": f"configs[1]: K synchronous msm_ctx_mult calls (per-MSM latency), window c={c}, points and "
+                    f"{K} scalar sets resident in HBM"}
+        # the same K sets through the pipelined batch (msm_ctx_mult_batch): throughput
+        pc.mult_batch(d16.data_ptr(), min(max(W, 1), K), 255, on_device=True, stream=sp)
+        torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        rb = pc.mult_batch(d16.data_ptr(), K, 255, on_device=True, stream=sp)
+        torch.cuda.synchronize(dev)
+        elb = time.perf_counter() - t
+        legs[f"cfg1_pippenger_2^16_batch_c{c}"] = {
+            "value": round(n16 * K / elb, 1), "unit": "pairs/s", "ms_per_step": round(elb / K * 1e3, 4),
+            "parity_vs_reference": m.compress(1, rb[0]).hex() == want16,
+            "batch_equals_sync": [m.compress(1, x) for x in rb] == [m.compress(1, x) for x in r],
+            "note": f"configs[1]: one msm_ctx_mult_batch call over the same {K} resident sets, window c={c}: front "
+                    f"k+2 beside accumulation k, two accumulation lanes, grouped reduction tails, host Horner of "
+                    f"group q beside the GPU work of later groups"}
         pc.close()
     for _ in range(max(W, 1)):
         dropin(1, P16, sets16[0], n16)
@@ -580,15 +599,17 @@ def config_legs(m, torch, dev, local, sp, pts, host, K, W):
         "parity_vs_reference": m.compress(1, r[0]).hex() == want10,
         "note": "the same 2^10 call through the GPU drop-in (launch/latency-bound at this size)"}
 
+    # ---- the blst-level CHES tile (main_p1.cpp:249-291 call sequence) at 2^16 and 2^20 ----
+    legs.update(tile_d_ches_legs(m, pts, host))
+
     # ---- configs[4]: G2 2^20 CHES batch ----
     t = time.time()
-    pts2 = m.fixed_points(2, n20)
+    pts2_host = m.fixed_points(2, n20)
     c2 = m.CHESContext(2, local, n_exp=20)
-    c2.build_table(pts2, n20, stream=sp)
+    c2.build_table(pts2_host, n20, stream=sp)
     c2.set_profiling(True)
     torch.cuda.synchronize(dev)
     setup = time.time() - t
-    del pts2
     k2 = min(K, 10)
     hptr, SS = host.data_ptr(), 32 * n20
     d2 = host[:k2 * SS].to(dev)
@@ -619,12 +640,104 @@ def config_legs(m, torch, dev, local, sp, pts, host, K, W):
         "setup_s": round(setup, 2),
         "note": f"configs[4]: G2 n=2^20 CHES (q=2^{par['q_exp']}, h={par['h']}, |B|={par['b_size']}), table in HBM, "
                 f"{k2} distinct scalar sets in pinned host memory, H2D in the timed region"}
+    # the G2 blst drop-in at 2^20 (main_p2.cpp:424 pippenger_blst_built_in): points + scalars per call
+    P2 = (ctypes.c_uint8 * (192 * n20)).from_buffer_copy(bytes(pts2_host))
+    S2 = set_bytes(0, n20)
+    dropin(2, P2, S2, n20)
+    r2, el2 = timed(lambda k: dropin(2, P2, S2, n20), 3)
+    legs["blst_p2s_mult_pippenger_2^20"] = {
+        "value": round(n20 * 3 / el2, 1), "unit": "pairs/s", "ms_per_step": round(el2 / 3 * 1e3, 4),
+        "parity_vs_reference": m.compress(2, r2[0]).hex() == _golden(m, 2, n20),
+        "note": "the G2 drop-in boundary (pippenger_blst_built_in of main_p2.cpp:400-436): per call 192 MiB of "
+                "points + 32 MiB of scalars from pageable host memory"}
+    del P2, pts2_host
     legs["cfg4_g2_ches_batch_resident"] = {
         "value": round(n20 * k2 / elr, 1), "unit": "pairs/s", "ms_per_step": round(elr / k2 * 1e3, 4),
         "parity_vs_reference": m.compress(2, br[0]).hex() == _golden(m, 2, n20),
         "note": "configs[4], the same sets resident in HBM"}
     c2.close()
     del d2
+    return legs
+
+
+def _std_digits(raw, n, q_exp, h):
+    """trans_uint256_t_to_standard_q_ary_expr (ref auxiliaryfunc.h:83-90) of n
+    32-byte scalars: n h ints, digit j of scalar i at i h + j, plus 2 pad slots
+    (main_p1.cpp:254)."""
+    import numpy as np
+    w = np.frombuffer(raw, dtype=np.uint64, count=4 * n).reshape(n, 4)
+    out = np.zeros(n * h + 2, dtype=np.int32)
+    mask = np.uint64((1 << q_exp) - 1)
+    for j in range(h):
+        o = q_exp * j
+        wi, sh = o // 64, o % 64
+        v = w[:, wi] >> np.uint64(sh)
+        if sh and wi + 1 < 4:
+            v = v | (w[:, wi + 1] << np.uint64(64 - sh))
+        out[j:n * h:h] = (v & mask).astype(np.int32)
+    return out
+
+
+def tile_d_ches_legs(m, pts, host):
+    """The blst-level CHES tile through the reference driver's method-2 call
+    sequence (main_p1.cpp:249-291): standard q-ary digits of every scalar,
+    blst_p1_construct_nh_scalars_nh_points (MB digits + one pointer per entry
+    into the host table T[3 n h], main_p1.cpp:155-172), then
+    blst_p1_tile_pippenger_d_CHES over the n h pointers -- the boundary hands the
+    table over by pointer, so every call gathers and uploads n h rows (1.2 GB
+    at 2^20) before the same GPU accumulation and reduction as the context.
+    Timed: the tile call; parity: set 0 against the golden MSM."""
+    import numpy as np
+    vp, sz, i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+    L = m.lib()
+    L.blst_p1_construct_nh_scalars_nh_points.argtypes = [vp, vp, vp, sz, vp, vp]
+    L.blst_p1_tile_pippenger_d_CHES.argtypes = [vp, vp, sz, vp, vp, vp, vp, vp, sz, i32]
+    legs = {}
+    hv = host.numpy()
+    for lg in (16, 20):
+        n = 1 << lg
+        ctx = m.CHESContext(1, 0, n_exp=lg)
+        ctx.build_table(bytes(pts)[:96 * n], n)
+        p = ctx.params
+        T = ctx.get_table()
+        ctx.mult(hv[:32 * n].tobytes())
+        t = time.perf_counter()
+        for _ in range(3):
+            ctx.mult(hv[:32 * n].tobytes())
+        sync_ms = (time.perf_counter() - t) / 3 * 1e3
+        ctx.close()
+        q, h = 1 << p["q_exp"], p["h"]
+        B = m.ches.bucket_set(q, p["a_h"])
+        H = m.ches.digit_table(q, p["a_h"])
+        Bn = np.frombuffer(B, dtype=np.int32)
+        v2i_np = np.zeros(int(Bn[-1]) + 1, dtype=np.int32)
+        v2i_np[Bn] = np.arange(len(Bn), dtype=np.int32)
+        v2i = (ctypes.c_int * len(v2i_np)).from_buffer_copy(v2i_np.tobytes())
+        ne = n * h
+        t0 = time.perf_counter()
+        nh_np = _std_digits(hv[:32 * n].tobytes(), n, p["q_exp"], h)
+        nh = (ctypes.c_int * len(nh_np)).from_buffer_copy(nh_np.tobytes())
+        signs = (ctypes.c_ubyte * ne)()
+        ptrs = (ctypes.c_void_p * ne)()
+        L.blst_p1_construct_nh_scalars_nh_points(nh, signs, ptrs, ne, T, H)
+        prep = time.perf_counter() - t0
+        buckets = (ctypes.c_uint8 * (192 * len(B)))()
+        ret = (ctypes.c_uint8 * 144)()
+        L.blst_p1_tile_pippenger_d_CHES(ret, ptrs, ne, nh, signs, buckets, B, v2i, len(B), p["d_max"])
+        reps = 3
+        t = time.perf_counter()
+        for _ in range(reps):
+            L.blst_p1_tile_pippenger_d_CHES(ret, ptrs, ne, nh, signs, buckets, B, v2i, len(B), p["d_max"])
+        el = (time.perf_counter() - t) / reps
+        legs[f"blst_p1_tile_pippenger_d_CHES_2^{lg}"] = {
+            "value": round(n / el, 1), "unit": "pairs/s", "ms_per_step": round(el * 1e3, 4),
+            "ctx_sync_ms": round(sync_ms, 4), "ratio_vs_ctx_sync": round(el * 1e3 / sync_ms, 2),
+            "host_prep_ms": round(prep * 1e3, 1), "entries": ne, "gathered_bytes": ne * 96,
+            "parity_vs_reference": m.compress(1, bytes(ret)).hex() == _golden(m, 1, n),
+            "note": f"main_p1.cpp:249-291 sequence (q=2^{p['q_exp']}, h={h}): digits + construct_nh (host, not timed), "
+                    f"then the timed blst_p1_tile_pippenger_d_CHES over {ne} row pointers into the host table; the "
+                    f"context's synchronous MSM on the same set for comparison (ctx_sync_ms, scalars H2D)"}
+        del T, ptrs, nh, signs, buckets
     return legs
 
 

@@ -212,6 +212,14 @@ int msm_ctx_set_points(msm_ctx *ctx, const void *points_affine, size_t npoints, 
  * on host or device; ret: blst_p1 / blst_p2 Jacobian (host memory) */
 int msm_ctx_mult(msm_ctx *ctx, void *ret, const byte *scalars, size_t stride, size_t nbits, int scalars_on_device,
                  void *hip_stream);
+/* `count` MSMs over the context's points in one pipelined call (extension: the
+ * shape of a prover committing many polynomials to one SRS; ref
+ * main_p1.cpp:470-476 runs 5 scalar arrays back to back): scalar set k at
+ * scalars + k * set_stride, each npoints strings of `stride` bytes; rets: count
+ * Jacobians.  scalars_on_device = 0: the sets are uploaded first.  Results equal
+ * `count` msm_ctx_mult calls. */
+int msm_ctx_mult_batch(msm_ctx *ctx, void *rets, const byte *scalars, size_t stride, size_t set_stride,
+                       size_t nbits, size_t count, int scalars_on_device, void *hip_stream);
 int msm_ctx_set_profiling(msm_ctx *ctx, int on);
 /* per-phase device ms of the last msm_ctx_mult (profiling on):
  * [digits, sort, accumulate, reduce, finalize, total] */

@@ -130,6 +130,19 @@ class MSMContext:
         check(lib().msm_ctx_mult(self._ctx, ret, ptr, stride, nbits, int(bool(on_device)), stream))
         return bytes(ret)
 
+    def mult_batch(self, scalars, count, nbits=255, stride=32, set_stride=None, on_device=False, stream=None):
+        """`count` pipelined MSMs (scalar set k at k * set_stride bytes); returns a
+        list of Jacobian byte strings, equal to `count` mult() calls."""
+        if set_stride is None:
+            set_stride = self.n * stride
+        nb = JAC_BYTES[self.group]
+        rets = (ctypes.c_uint8 * (nb * count))()
+        ptr = scalars if on_device else _buf(scalars)
+        check(lib().msm_ctx_mult_batch(self._ctx, rets, ptr, stride, set_stride, nbits, count, int(bool(on_device)),
+                                       stream))
+        raw = bytes(rets)
+        return [raw[k * nb:(k + 1) * nb] for k in range(count)]
+
     def set_profiling(self, on=True):
         check(lib().msm_ctx_set_profiling(self._ctx, int(on)))
 

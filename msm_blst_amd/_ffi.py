@@ -45,6 +45,7 @@ def lib():
     L.msm_ctx_create.argtypes = [ctypes.POINTER(vp), i32, i32, i32]
     L.msm_ctx_set_points.argtypes = [vp, vp, sz, i32, vp]
     L.msm_ctx_mult.argtypes = [vp, vp, vp, sz, sz, i32, vp]
+    L.msm_ctx_mult_batch.argtypes = [vp, vp, vp, sz, sz, sz, sz, i32, vp]
     L.msm_ctx_set_profiling.argtypes = [vp, i32]
     L.msm_ctx_phase_times.argtypes = [vp, vp]
     L.msm_ctx_destroy.argtypes = [vp]

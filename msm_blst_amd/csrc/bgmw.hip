@@ -99,8 +99,12 @@ void Bgmw<G>::build_table(const void *pts, size_t n, bool on_device, hipStream_t
   pref.ensure(K * chunk * sizeof(F));
   for (size_t i0 = 0; i0 < n; i0 += chunk) {
     size_t cnt = std::min(chunk, n - i0);
-    hipLaunchKernelGGL((k_ches_table<G, 1>), dim3(nblk(cnt, 64)), dim3(64), 0, s, base.as<Aff<F>>(), i0, cnt, q_exp_,
-                       h_, scratch.as<Xyzz<F>>(), pref.as<F>(), table_.as<AffP<F>>());
+    if constexpr (G == 2)  // lane pairs (pair_kernels.hpp)
+      hipLaunchKernelGGL((k_ches_table2p<1>), dim3(nblk(2 * cnt, 128)), dim3(128), 0, s, base.as<Aff<F>>(), i0, cnt,
+                         q_exp_, h_, scratch.as<Xyzz<F>>(), pref.as<F>(), table_.as<AffP<F>>());
+    else
+      hipLaunchKernelGGL((k_ches_table<G, 1>), dim3(nblk(cnt, 64)), dim3(64), 0, s, base.as<Aff<F>>(), i0, cnt, q_exp_,
+                         h_, scratch.as<Xyzz<F>>(), pref.as<F>(), table_.as<AffP<F>>());
     MSM_HIP_CHECK(hipGetLastError());
   }
   MSM_HIP_CHECK(hipStreamSynchronize(s));

@@ -233,11 +233,19 @@ void WeightedReducer<G>::plan(const std::vector<uint32_t> &w, const std::vector<
   }
   // level 0 + pairwise levels
   std::vector<uint32_t> cur_seg = seg;
-  static const int C0 = [] {
+  // Level-0 chunk length: a chunk of C items is C - 1 dependent adds in one
+  // lane.  Large plans keep 8 (few lanes per item, fewest levels); small ones
+  // (a few hundred thousand items: plain Pippenger at 2^16, CHES shards of
+  // 2^17..2^19) would leave the chip < 1 wave per SIMD deep with 7-add chains
+  // (the 2^16 level 0 ran 103 us for 311 K adds, profiles/r04_fixed_cost.txt),
+  // so they take 4 or 2 and one or two more (tail) levels.  The adds are the
+  // same in total (items - segments); MSM_L0_CHUNK=<2..64> overrides.
+  static const int C0env = [] {
     const char *e = getenv("MSM_L0_CHUNK");  // A/B knob: level-0 chunk length
-    return e ? std::max(2, std::min(64, atoi(e))) : 8;
+    return e ? std::max(2, std::min(64, atoi(e))) : 0;
   }();
-  int C = C0;
+  const size_t lane_items = idx.size() * (G == 2 ? 2 : 1);  // G2 segment sums run on lane pairs
+  int C = C0env ? C0env : lane_items >= ((size_t)3 << 19) ? 8 : lane_items >= ((size_t)600 << 10) ? 4 : 2;
   while (true) {
     std::vector<uint32_t> st, nseg;
     size_t k = 0;
@@ -493,6 +501,38 @@ std::vector<hfp::Jac<typename HostField<G>::F>> WeightedReducer<G>::read_windows
   return combine(host.data());
 }
 
+template <int G>
+hfp::Jac<typename HostField<G>::F> WeightedReducer<G>::combine_windows(const void *host, int c) const {
+  const hfp::Jac<HF> *T = reinterpret_cast<const hfp::Jac<HF> *>(host);
+  // terms (exponent, point): L_w at c w, H_w at c w + s; Horner from the top
+  std::vector<std::pair<long, int>> terms;
+  for (int ww = 0; ww < nwin_; ++ww) {
+    terms.emplace_back((long)c * ww, 2 * ww);
+    terms.emplace_back((long)c * ww + sbits_, 2 * ww + 1);
+  }
+  std::sort(terms.begin(), terms.end());
+  hfp::Jac<HF> acc = T[terms.back().second];
+  long e = terms.back().first;
+  for (int k = (int)terms.size() - 2; k >= 0; --k) {
+    for (; e > terms[k].first; --e) acc = hfp::dbl(acc);
+    acc = hfp::addj(acc, T[terms[k].second]);
+  }
+  for (; e > 0; --e) acc = hfp::dbl(acc);
+  return acc;
+}
+
+template <int G>
+hfp::Jac<typename HostField<G>::F> WeightedReducer<G>::read_total(hipStream_t s, int c) {
+  if (bits_ && nout_.size() >= 2) {  // one-window plan ended in bit sums (launch_tail): its T_0 is the total
+    const std::vector<hfp::Jac<HF>> T = read_windows(s);
+    return horner(T, c);
+  }
+  std::vector<uint8_t> host(out_bytes());
+  copy_out(s, 0, host.data());
+  MSM_HIP_CHECK(hipStreamSynchronize(s));
+  return combine_windows(host.data(), c);
+}
+
 template class WeightedReducer<MSM_GROUP>;
 
 // ------------------------------------------------------------------ Ches --
@@ -593,8 +633,12 @@ void Ches<G>::build_table(const void *pts, size_t n, bool on_device, hipStream_t
   pref.ensure(K * chunk * sizeof(F));
   for (size_t i0 = 0; i0 < n; i0 += chunk) {
     size_t cnt = std::min(chunk, n - i0);
-    hipLaunchKernelGGL((k_ches_table<G, 3>), dim3(nblk(cnt, 64)), dim3(64), 0, s, base.as<Aff<F>>(), i0, cnt, p_.q_exp,
-                       p_.h, scratch.as<Xyzz<F>>(), pref.as<F>(), table_.as<AffP<F>>());
+    if constexpr (G == 2)  // lane pairs: no spills (pair_kernels.hpp)
+      hipLaunchKernelGGL((k_ches_table2p<3>), dim3(nblk(2 * cnt, 128)), dim3(128), 0, s, base.as<Aff<F>>(), i0, cnt,
+                         p_.q_exp, p_.h, scratch.as<Xyzz<F>>(), pref.as<F>(), table_.as<AffP<F>>());
+    else
+      hipLaunchKernelGGL((k_ches_table<G, 3>), dim3(nblk(cnt, 64)), dim3(64), 0, s, base.as<Aff<F>>(), i0, cnt,
+                         p_.q_exp, p_.h, scratch.as<Xyzz<F>>(), pref.as<F>(), table_.as<AffP<F>>());
     MSM_HIP_CHECK(hipGetLastError());
   }
   MSM_HIP_CHECK(hipStreamSynchronize(s));
@@ -836,22 +880,29 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
   // reallocate (a hipFree inside the pipelined region would synchronise it)
   // (both reducer sets, and both bucket sets, whatever this batch's length: a
   // short warm-up batch must leave nothing to allocate inside a longer one)
-  for (int t = 0; t < kBSets; ++t) red_.ensure_group(t, kGroup);
+  // front sets and reducer sets in rotation: the lane schedule (small MSMs,
+  // periods of a few hundred us) keeps fronts further ahead and lets group q
+  // reuse reducer set q % 4 after tail q - 4 (a tail is ~30 latency-bound
+  // launches, ~1 ms beside the accumulations: with 2 sets group q + 2 waited
+  // for it, profiles/r04_batch_trace_2p17.txt)
+  const int nfr = nl >= 2 ? kFrontsMax : kFronts, nred = nl >= 2 ? 4 : 2;
+  for (int t = 0; t < nred; ++t) red_.ensure_group(t, kGroup);
   // front sets sized for a whole front group (the sort's scan scratch too): run
   // one sort of fg_max sets per set before the loop if they are not yet sized
   // (fg_max dummy sets of all-zero scalars, outside the batch timing)
   const size_t sslot = n * stride;  // one device scalar slot
   bool unsized = false;
-  for (int f = 0; f < kFronts; ++f) unsized |= fs_[f].sorted.bytes < n * (size_t)p_.h * fg_max * 4;
+  for (int f = 0; f < nfr; ++f) unsized |= fs_[f].sorted.bytes < n * (size_t)p_.h * fg_max * 4;
   // host sets: nsg groups of fg_max device slots, copied up to nsg groups ahead
   // (4 single-set groups -- as the round-2 pipeline's four slots -- or 2 larger)
   static const size_t nsg_env = [] {
     const char *e = getenv("MSM_H2D_SLOTS");  // A/B knob: slot groups (copies issued that far ahead)
     return (size_t)(e ? std::max(2, std::min(256, atoi(e))) : 0);
   }();
-  const size_t nsg = nsg_env ? nsg_env : fg_max == 1 ? 4 : 2;
+  // (every group's copies are enqueued before its front: nsg >= nfr - 1)
+  const size_t nsg = std::max<size_t>(nsg_env ? nsg_env : fg_max == 1 ? 4 : 2, (size_t)nfr - 1);
   if (scalars_on_host || unsized) scal_.ensure(std::max<size_t>(nsg, 2) * fg_max * sslot + 16);
-  for (int f = 0; f < kFronts; ++f)
+  for (int f = 0; f < nfr; ++f)
     if (fs_[f].sorted.bytes < n * (size_t)p_.h * fg_max * 4) {
       MSM_HIP_CHECK(hipMemsetAsync(scal_.p, 0, fg_max * sslot, s));
       digits_sort(s, scal_.as<uint8_t>(), stride, sslot, (int)fg_max, f);
@@ -865,7 +916,7 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
       MSM_HIP_CHECK(hipEventCreate(&e));
       acc_ev_.push_back(e);
     }
-  // Streams, front groups g (front set g % kFronts), bucket sets k % kBSets and,
+  // Streams, front groups g (front set g % nfr), bucket sets k % kBSets and,
   // for host scalars, nsg groups of device scalar slots (g % nsg):
   //   fstream_:  digits + sort of front group g: ONE pass per stage over its R_g
   //              scalar sets (bucket_sort.hpp), after group g - 3's accumulations
@@ -925,19 +976,17 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
     if (g >= nfg) return;
     const bool copied = scalars_on_host && !zero_copy;
     if (copied) MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, evc[g], 0));
-    if (g >= (size_t)kFronts) {  // front set g % kFronts: every accumulation of group g - kFronts has read it
-      const size_t last = fgb[g - kFronts + 1] - 1;
+    if (g >= (size_t)nfr) {  // front set g % nfr: every accumulation of group g - nfr has read it
+      const size_t last = fgb[g - nfr + 1] - 1;
       MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, eva[last], 0));
-      for (size_t d = 1; d < (size_t)nl && last >= d && last - d >= fgb[g - kFronts]; ++d)  // its other lanes
+      for (size_t d = 1; d < (size_t)nl && last >= d && last - d >= fgb[g - nfr]; ++d)  // its other lanes
         MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, eva[last - d], 0));
     }
     const uint8_t *src = copied ? slots(g) : scalars + fgb[g] * set_stride;
-    digits_sort(fstream_, src, stride, copied ? sslot : set_stride, (int)(fgb[g + 1] - fgb[g]), (int)(g % kFronts));
+    digits_sort(fstream_, src, stride, copied ? sslot : set_stride, (int)(fgb[g + 1] - fgb[g]), (int)(g % nfr));
     MSM_HIP_CHECK(hipEventRecord(evf[g], fstream_));
   };
   for (size_t g = 0; g < nsg; ++g) copy_group(g);
-  // every group's copies are enqueued before its front (nsg >= kFronts - 1)
-  static_assert(kFronts - 1 <= 2, "copy lead must cover the front lead");
   // Accumulation k waits for level 0 of MSM k - 1, so level 0 runs beside the
   // fronts, never beside the next accumulation.  Without this wait the batch
   // fell, in about one run in three, into a schedule where fronts ran two MSMs
@@ -954,7 +1003,7 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
     return e ? (atoi(e) != 0 ? 1 : 0) : -1;
   }();
   const bool l0_first = l0_env < 0 ? G == 1 : l0_env == 1;
-  for (size_t g = 0; g + 1 < (size_t)kFronts; ++g) front_group(g);
+  for (size_t g = 0; g + 1 < (size_t)nfr; ++g) front_group(g);
   // Two accumulation lanes (small MSMs, batch_lanes()): MSM k accumulates into
   // bucket set k % 2 on lane stream k % 2 (the caller's s, tails_[0]) and its
   // level 0 follows on the same stream, so accumulations k and k + 1 run side
@@ -970,15 +1019,16 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
     hipStream_t lane[3] = {s, tails_[0], tails_[1]}, ts = nl == 3 ? fstream_ : tails_[1];
     for (size_t g = 0; g < nfg; ++g) {
       copy_group(g + nsg);
-      front_group(g + kFronts - 1);
+      front_group(g + nfr - 1);
       for (size_t k = fgb[g]; k < fgb[g + 1]; ++k) {
         hipStream_t L = lane[k % nl];
-        const int bset = (int)(k % nl), slot = (int)(k % R), gset = (int)((k / R) % 2);
         const size_t q = k / R;
+        const int bset = (int)(k % nl), slot = (int)(k % R), gset = (int)(q % nred);
         MSM_HIP_CHECK(hipStreamWaitEvent(L, evf[g], 0));
-        if (q >= 2 && slot < nl) MSM_HIP_CHECK(hipStreamWaitEvent(L, evt[q - 2], 0));  // reducer set q % 2 free
+        if (q >= (size_t)nred && slot < nl)  // reducer set q % nred free again
+          MSM_HIP_CHECK(hipStreamWaitEvent(L, evt[q - nred], 0));
         if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k], L));
-        accumulate(L, (int)(g % kFronts), (int)(k - fgb[g]), bset);
+        accumulate(L, (int)(g % nfr), (int)(k - fgb[g]), bset);
         if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k + 1], L));
         MSM_HIP_CHECK(hipEventRecord(eva[k], L));
         red_.launch_head_slot(L, buckets_[bset].p, gset, slot);
@@ -994,7 +1044,7 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
   }
   for (size_t g = 0; g < (nl >= 2 ? 0 : nfg); ++g) {
     copy_group(g + nsg);
-    front_group(g + kFronts - 1);  // may start as soon as group g - 1's accumulations release its front set
+    front_group(g + nfr - 1);  // may start as soon as group g - 1's accumulations release its front set
     MSM_HIP_CHECK(hipStreamWaitEvent(s, evf[g], 0));
     for (size_t k = fgb[g]; k < fgb[g + 1]; ++k) {
       const int bset = (int)(k % kBSets), slot = (int)(k % R), gset = (int)((k / R) % 2);
@@ -1002,7 +1052,7 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
       if (k >= (size_t)kBSets) MSM_HIP_CHECK(hipStreamWaitEvent(s, evh[k - kBSets], 0));  // bucket set free again
       if (l0_first && k >= 1) MSM_HIP_CHECK(hipStreamWaitEvent(s, evh[k - 1], 0));
       if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k], s));
-      accumulate(s, (int)(g % kFronts), (int)(k - fgb[g]), bset);
+      accumulate(s, (int)(g % nfr), (int)(k - fgb[g]), bset);
       if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k + 1], s));
       MSM_HIP_CHECK(hipEventRecord(eva[k], s));
       MSM_HIP_CHECK(hipStreamWaitEvent(ts, eva[k], 0));

@@ -27,26 +27,33 @@ namespace msm {
 constexpr uint32_t CH_IDX_MASK = 0x00ffffffu;
 
 // ---------------------------------------------------------------- inversion --
-// a^(p-2) mod p (Fermat), fixed 4-bit windows, input any lazy value, output S.
+// a^(p-2) mod p (Fermat), fixed 2-bit windows, input any lazy value, output S.
+// Inlined and register-lean (a, a^2, a^3 and the accumulator: ~60 VGPRs): the
+// earlier 4-bit version kept a 16-entry table in scratch (912 B/lane) and was
+// a call -- the table kernels that use it are now scratch-free.
+// One inversion per lane amortises over the lane's 3h table rows, so its ~570
+// products (vs ~490 with 4-bit windows) do not matter.
 __device__ constexpr uint64_t PM2[6] = {0xb9feffffffffaaa9ull, 0x1eabfffeb153ffffull, 0x6730d2a0f6b0f624ull,
                                         0x64774b84f38512bfull, 0x4b1ba7b6434bacd7ull, 0x1a0111ea397fe69aull};
-static __device__ __noinline__ void fp_inv(Fp &r, const Fp &a) {
-  Fp tab[16];
-  fp_one(tab[0]);
-  tab[1] = a;
-  fp_norm(tab[1]);
-  for (int k = 2; k < 16; ++k) fp_mul(tab[k], tab[k - 1], tab[1]);
-  Fp acc;
+__device__ __forceinline__ void fp_inv(Fp &r, const Fp &a) {
+  Fp a1 = a, a2, a3, acc;
+  fp_norm(a1);
+  fp_sqr(a2, a1);
+  fp_mul(a3, a2, a1);
   fp_one(acc);
-  for (int nib = 95; nib >= 0; --nib) {
-    if (nib != 95) {
-      for (int k = 0; k < 4; ++k) fp_sqr(acc, acc);
+  for (int k = 190; k >= 0; --k) {  // 2-bit windows of p - 2 (381 bits), from the top
+    if (k != 190) {
+      fp_sqr(acc, acc);
+      fp_sqr(acc, acc);
     }
-    uint32_t w = (uint32_t)(PM2[nib >> 4] >> ((nib & 15) * 4)) & 15u;
-    Fp t = tab[0];
-    for (int k = 1; k < 16; ++k)
-      if ((uint32_t)k == w) t = tab[k];  // uniform per exponent nibble
-    fp_mul(acc, acc, t);
+    const uint32_t w = (uint32_t)(PM2[k >> 5] >> ((k & 31) * 2)) & 3u;  // uniform: the exponent is a constant
+    if (w) {
+      const uint32_t m1 = 0u - (uint32_t)(w == 1), m2 = 0u - (uint32_t)(w == 2), m3 = 0u - (uint32_t)(w == 3);
+      Fp t;
+#pragma unroll
+      for (int i = 0; i < NL; ++i) t.v[i] = (a1.v[i] & m1) | (a2.v[i] & m2) | (a3.v[i] & m3);
+      fp_mul(acc, acc, t);
+    }
   }
   r = acc;
 }
@@ -100,13 +107,12 @@ static __global__ void __launch_bounds__(256)
   xyzz_from_aff(Q, p, false);
   for (int j = 0; j < h; ++j) {
     st16(&scratch[(size_t)(M * j) * cnt + t], Q);
-    if (M == 3) {
-      Xyzz<F> Q2, Q3;
-      xyzz_dbl(Q2, Q);
-      Q3 = Q2;
-      xyzz_add(Q3, Q);
-      st16(&scratch[(size_t)(3 * j + 1) * cnt + t], Q2);
-      st16(&scratch[(size_t)(3 * j + 2) * cnt + t], Q3);
+    if (M == 3) {  // 2 Q, then 3 Q = 2 Q + Q in place (one point fewer live)
+      Xyzz<F> R;
+      xyzz_dbl(R, Q);
+      st16(&scratch[(size_t)(3 * j + 1) * cnt + t], R);
+      xyzz_add(R, Q);
+      st16(&scratch[(size_t)(3 * j + 2) * cnt + t], R);
     }
     if (j + 1 < h)
       for (int e = 0; e < q_exp; ++e) {

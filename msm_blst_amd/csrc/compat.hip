@@ -16,6 +16,7 @@
 
 #include "ches_kernels.hpp"
 #include "engine.hpp"
+#include "hoststage.hpp"
 #include "pair_kernels.hpp"
 #include "pool.hpp"
 
@@ -25,14 +26,44 @@
 
 namespace msm {
 
+// page-locked host staging of the pointer-array tiles (entry_msm_ptrs)
+struct PinnedBuf {
+  void *p = nullptr;
+  size_t bytes = 0;
+  PinnedBuf() = default;
+  PinnedBuf(const PinnedBuf &) = delete;
+  PinnedBuf &operator=(const PinnedBuf &) = delete;
+  ~PinnedBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+  void ensure(size_t b) {  // callers synchronise the stream that reads it first
+    if (b <= bytes) return;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    bytes = 0;
+    MSM_HIP_CHECK(hipHostMalloc(&p, b, hipHostMallocDefault));
+    bytes = b;
+  }
+  template <class T>
+  T *as() const {
+    return reinterpret_cast<T *>(p);
+  }
+};
+
 template <int G>
 struct EntryMsmState {
   DevBuf pts, keys, vals, sorted, counts, offsets, order, buckets, xfer, bx;
   BucketSort sort;
   WeightedReducer<G> red;
   std::vector<uint32_t> planned;  // weights the reducer plan was built for
-  size_t device_bytes() const {
-    size_t b = 0;
+  PinnedBuf hkv, hring, hbx;      // pinned: keys + vals, the point-row ring, exported buckets
+  hipEvent_t ring_ev[4] = {};
+  ~EntryMsmState() {
+    for (hipEvent_t &e : ring_ev)
+      if (e) (void)hipEventDestroy(e);
+  }
+  size_t device_bytes() const {  // device buffers + pinned staging (the pool's idle budget counts both)
+    size_t b = hkv.bytes + hring.bytes + hbx.bytes;
     for (const DevBuf *d : {&pts, &keys, &vals, &sorted, &counts, &offsets, &order, &buckets, &xfer, &bx}) b += d->bytes;
     return b;
   }
@@ -52,6 +83,10 @@ static void plan_if_changed(EntryMsmState<G> &S, const uint32_t *w, size_t nb) {
   S.planned.assign(w, w + nb);
   S.red.plan(S.planned);
 }
+
+template <int G>
+static void entry_msm_back(EntryMsmState<G> &S, hipStream_t s, void *ret, size_t ne, size_t nb,
+                           const uint32_t *weights, void *buckets_out, bool pinned_export);
 
 template <int G>
 void entry_msm(void *ret, const void *pts_blst, size_t npts, const uint32_t *keys, const uint32_t *vals, size_t ne,
@@ -83,6 +118,17 @@ void entry_msm(void *ret, const void *pts_blst, size_t npts, const uint32_t *key
     MSM_HIP_CHECK(hipMemcpyAsync(S.keys.p, keys, ne * 4, hipMemcpyHostToDevice, s));
     MSM_HIP_CHECK(hipMemcpyAsync(S.vals.p, vals, ne * 4, hipMemcpyHostToDevice, s));
   }
+  entry_msm_back<G>(S, s, ret, ne, nb, weights, buckets_out, false);
+}
+
+// sort + accumulate + (bucket export) + weighted reduction of the entries in
+// S.keys / S.vals over the points in S.pts
+template <int G>
+static void entry_msm_back(EntryMsmState<G> &S, hipStream_t s, void *ret, size_t ne, size_t nb,
+                           const uint32_t *weights, void *buckets_out, bool pinned_export) {
+  typedef typename FieldOf<G>::F F;
+  typedef typename HostField<G>::F HF;
+  hfp::Jac<HF> out;
   S.counts.ensure(nb * 4);
   S.offsets.ensure(nb * 4);
   S.order.ensure(nb * 4);
@@ -93,17 +139,83 @@ void entry_msm(void *ret, const void *pts_blst, size_t npts, const uint32_t *key
                        S.pts.template as<Aff<F>>(),
                        S.buckets.template as<Xyzz<F>>(), nb);
   MSM_HIP_CHECK(hipGetLastError());
+  plan_if_changed(S, weights, nb);
+  S.red.launch(s, S.buckets.p);
   if (buckets_out) {
     S.bx.ensure(nb * 192 * G);
     hipLaunchKernelGGL(k_export_xyzz<G>, dim3(nblk(nb, 256)), dim3(256), 0, s, S.buckets.template as<Xyzz<F>>(),
                        S.bx.template as<uint64_t>(), nb);
     MSM_HIP_CHECK(hipGetLastError());
-    MSM_HIP_CHECK(hipMemcpyAsync(buckets_out, S.bx.p, nb * 192 * G, hipMemcpyDeviceToHost, s));
+    if (pinned_export) {  // DMA into page-locked memory, then a parallel copy into the caller's buckets
+      S.hbx.ensure(nb * 192 * G);
+      MSM_HIP_CHECK(hipMemcpyAsync(S.hbx.p, S.bx.p, nb * 192 * G, hipMemcpyDeviceToHost, s));
+    } else {
+      MSM_HIP_CHECK(hipMemcpyAsync(buckets_out, S.bx.p, nb * 192 * G, hipMemcpyDeviceToHost, s));
+    }
   }
-  plan_if_changed(S, weights, nb);
-  S.red.launch(s, S.buckets.p);
   out = S.red.read(s);
+  if (buckets_out && pinned_export) parallel_memcpy(buckets_out, S.hbx.p, nb * 192 * G);
   std::memcpy(ret, &out, sizeof out);
+}
+
+template <int G>
+void entry_msm_ptrs(void *ret, const void *const *points, size_t ne, EntryFill fill, void *fill_ctx, size_t nb,
+                    const uint32_t *weights, void *buckets_out) {
+  typedef typename FieldOf<G>::F F;
+  typedef typename HostField<G>::F HF;
+  if (nb == 0 || ne == 0) {
+    hfp::Jac<HF> out;
+    std::memset(&out, 0, sizeof out);
+    if (ne == 0 && nb && buckets_out) std::memset(buckets_out, 0, nb * 192 * G);
+    std::memcpy(ret, &out, sizeof out);
+    return;
+  }
+  if (ne >= (1ull << 31)) throw std::runtime_error("entry MSM too large");
+  auto lease = entry_state<G>();
+  EntryMsmState<G> &S = **lease;
+  hipStream_t s = lease->stream();
+  MSM_HIP_CHECK(hipStreamSynchronize(s));  // the pinned buffers are free (no DMA of an earlier call pending)
+  const size_t psz = 96 * G;
+  // keys / vals: filled in parallel straight into pinned memory, one DMA each
+  S.hkv.ensure(ne * 8);
+  uint32_t *hk = S.hkv.template as<uint32_t>(), *hv = hk + ne;
+  const size_t piece = std::max<size_t>((size_t)1 << 16, (ne + 63) / 64);
+  WorkerPool::get().parallel_for((ne + piece - 1) / piece, [&](size_t c) {
+    const size_t t0 = c * piece, t1 = std::min(ne, t0 + piece);
+    fill(fill_ctx, t0, t1, hk + t0, hv + t0);
+  });
+  S.keys.ensure(ne * 4);
+  S.vals.ensure(ne * 4);
+  S.sorted.ensure(ne * 4 + 64);  // + the accumulation's payload window
+  MSM_HIP_CHECK(hipMemcpyAsync(S.keys.p, hk, ne * 4, hipMemcpyHostToDevice, s));
+  MSM_HIP_CHECK(hipMemcpyAsync(S.vals.p, hv, ne * 4, hipMemcpyHostToDevice, s));
+  // point rows: gathered chunk by chunk into a 4-slot pinned ring (the host
+  // gather of chunk c + 1 overlaps the DMA of chunk c), converted on the device
+  constexpr int kSlots = 4;
+  const size_t chunk = std::min(ne, std::max<size_t>(((size_t)16 << 20) / psz, (ne + kSlots - 1) / kSlots / 4 + 1));
+  S.hring.ensure(chunk * psz * kSlots);
+  for (hipEvent_t &e : S.ring_ev)
+    if (!e) MSM_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  S.xfer.ensure(ne * psz);
+  S.pts.ensure(ne * sizeof(Aff<F>));
+  bool used[kSlots] = {};
+  for (size_t c0 = 0, k = 0; c0 < ne; c0 += chunk, k = (k + 1) % kSlots) {
+    const size_t cnt = std::min(chunk, ne - c0);
+    if (used[k]) MSM_HIP_CHECK(hipEventSynchronize(S.ring_ev[k]));
+    uint8_t *slot = S.hring.template as<uint8_t>() + k * chunk * psz;
+    const size_t sub = std::max<size_t>(4096, (cnt + 15) / 16);
+    WorkerPool::get().parallel_for((cnt + sub - 1) / sub, [&](size_t j) {
+      const size_t a = j * sub, b = std::min(cnt, a + sub);
+      for (size_t t = a; t < b; ++t) std::memcpy(slot + t * psz, points[c0 + t], psz);
+    });
+    MSM_HIP_CHECK(hipMemcpyAsync(S.xfer.template as<uint8_t>() + c0 * psz, slot, cnt * psz, hipMemcpyHostToDevice, s));
+    MSM_HIP_CHECK(hipEventRecord(S.ring_ev[k], s));
+    used[k] = true;
+  }
+  hipLaunchKernelGGL(k_convert_points<G>, dim3(nblk(ne, 256)), dim3(256), 0, s, S.xfer.template as<uint64_t>(),
+                     S.pts.template as<Aff<F>>(), ne);
+  MSM_HIP_CHECK(hipGetLastError());
+  entry_msm_back<G>(S, s, ret, ne, nb, weights, buckets_out, true);
 }
 
 // sum_i w_i buckets[i] for caller-filled blst xyzz buckets
@@ -135,5 +247,7 @@ void weighted_bucket_sum(void *ret, const void *buckets_blst, size_t nb, const u
 template void entry_msm<MSM_GROUP>(void *, const void *, size_t, const uint32_t *, const uint32_t *, size_t, size_t,
                                    const uint32_t *, void *);
 template void weighted_bucket_sum<MSM_GROUP>(void *, const void *, size_t, const uint32_t *);
+template void entry_msm_ptrs<MSM_GROUP>(void *, const void *const *, size_t, EntryFill, void *, size_t,
+                                        const uint32_t *, void *);
 
 }  // namespace msm

@@ -99,6 +99,13 @@ Pippenger<G>::Pippenger(int device, int window_bits) : dev_(device), c_(window_b
 template <int G>
 Pippenger<G>::~Pippenger() {
   for (auto &e : ev_) (void)hipEventDestroy(e);
+  for (auto &e : bev_) (void)hipEventDestroy(e);
+  for (hipStream_t q : {fstream_, lane1_, tstream_})
+    if (q) {
+      (void)hipStreamSynchronize(q);
+      (void)hipStreamDestroy(q);
+    }
+  if (host_out_) (void)hipHostFree(host_out_);
   if (up_) {
     (void)hipStreamSynchronize(up_);
     (void)hipStreamDestroy(up_);
@@ -110,9 +117,9 @@ Pippenger<G>::~Pippenger() {
 template <int G>
 size_t Pippenger<G>::device_bytes() const {
   size_t b = stage_ ? stage_->pinned_bytes() : 0;
-  for (const DevBuf *d : {&pts_, &keys_, &vals_, &counts_, &offsets_, &sorted_, &order_, &buckets_, &tmp_, &scal_})
-    b += d->bytes;
-  return b + sort_.device_bytes();
+  for (const DevBuf *d : {&pts_, &buckets_[0], &buckets_[1], &tmp_, &scal_}) b += d->bytes;
+  for (const ChesFrontSet &f : fs_) b += f.device_bytes();
+  return b;
 }
 
 template <int G>
@@ -159,61 +166,76 @@ static void launch_digits(hipStream_t s, const uint8_t *sc, size_t stride, size_
   }
 
 template <int G>
-void Pippenger<G>::front(hipStream_t s, const uint8_t *d_scalars, size_t stride, int nbits, const uint8_t *neg) {
+void Pippenger<G>::front(hipStream_t s, const uint8_t *d_scalars, size_t stride, int nbits, const uint8_t *neg,
+                         ChesFrontSet &f) {
   const int c = c_;
   const int W = (nbits + 1 + c - 1) / c;
   const size_t NB = (size_t)1 << (c - 1);
   const size_t NT = (size_t)W * NB;
   const size_t n = n_, ne = (size_t)W * n;
-  keys_.ensure(ne * 4);
-  vals_.ensure(ne * 4);
-  sorted_.ensure(ne * 4 + 64);  // + the accumulation's 16-B payload window past a run's end
-  counts_.ensure(NT * 4);
-  offsets_.ensure(NT * 4);
-  order_.ensure(NT * 4);
-  if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[0], s));
-  MSM_C_DISPATCH(c, launch_digits, s, d_scalars, stride, n, nbits, W, keys_.as<uint32_t>(), vals_.as<uint32_t>(), neg,
+  f.keys.ensure(ne * 4);
+  f.vals.ensure(ne * 4);
+  f.sorted.ensure(ne * 4 + 64);  // + the accumulation's 16-B payload window past a run's end
+  f.counts.ensure(NT * 4);
+  f.offsets.ensure(NT * 4);
+  f.order.ensure(NT * 4);
+  const bool prof = profile_ && &f == &fs_[0];
+  if (prof) MSM_HIP_CHECK(hipEventRecord(ev_[0], s));
+  MSM_C_DISPATCH(c, launch_digits, s, d_scalars, stride, n, nbits, W, f.keys.as<uint32_t>(), f.vals.as<uint32_t>(), neg,
                  top_copies_log2(nbits));
   MSM_HIP_CHECK(hipGetLastError());
-  if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[1], s));
-  sort_.run(s, keys_.as<uint32_t>(), vals_.as<uint32_t>(), ne, (uint32_t)NT, sorted_.as<uint32_t>(),
-            counts_.as<uint32_t>(), offsets_.as<uint32_t>(), order_.as<uint32_t>());
-  if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[2], s));
+  if (prof) MSM_HIP_CHECK(hipEventRecord(ev_[1], s));
+  f.sort.run(s, f.keys.as<uint32_t>(), f.vals.as<uint32_t>(), ne, (uint32_t)NT, f.sorted.as<uint32_t>(),
+             f.counts.as<uint32_t>(), f.offsets.as<uint32_t>(), f.order.as<uint32_t>());
+  if (prof) MSM_HIP_CHECK(hipEventRecord(ev_[2], s));
 }
 
 template <int G>
-void Pippenger<G>::back(hipStream_t s, int nbits, hfp::Jac<HF> *out) {
+void Pippenger<G>::accumulate(hipStream_t s, int nbits, ChesFrontSet &f, DevBuf &bk) {
   typedef typename FieldOf<G>::F F;
+  const int W = (nbits + 1 + c_ - 1) / c_;
+  const size_t NT = (size_t)W << (c_ - 1);
+  bk.ensure(NT * sizeof(Xyzz<F>));
+  launch_accumulate<G>(s, f.sort.sched(f.order.as<uint32_t>(), f.sorted.as<uint32_t>(), 0, NT), pts_.as<Aff<F>>(),
+                       bk.as<Xyzz<F>>(), NT);
+  MSM_HIP_CHECK(hipGetLastError());
+}
+
+template <int G>
+void Pippenger<G>::plan_reduction(int nbits) {
   const int c = c_;
   const int W = (nbits + 1 + c - 1) / c;
   const size_t NB = (size_t)1 << (c - 1);
   const size_t NT = (size_t)W * NB;
-  buckets_.ensure(NT * sizeof(Xyzz<F>));
-  launch_accumulate<G>(s, sort_.sched(order_.as<uint32_t>(), sorted_.as<uint32_t>(), 0, NT), pts_.as<Aff<F>>(),
-                       buckets_.as<Xyzz<F>>(), NT);
-  MSM_HIP_CHECK(hipGetLastError());
-  if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[3], s));
   const int tcl = top_copies_log2(nbits);
-  if (red_W_ != W || red_tcl_ != tcl) {  // bucket (w, b-1) has weight b in window w; plan once per layout
-    std::vector<uint32_t> wt(NT), win(NT);
-    const size_t ntop = NB >> tcl;  // top window: slot k holds a copy of bucket (k mod ntop) + 1
-    for (size_t k = 0; k < NT; ++k) {
-      const size_t w = k / NB, b = k % NB;
-      wt[k] = (uint32_t)((w == (size_t)W - 1 ? b % ntop : b) + 1);
-      win[k] = (uint32_t)w;
-    }
-    red_.plan(wt, win, W);
-    red_W_ = W;
-    red_tcl_ = tcl;
+  if (red_W_ == W && red_tcl_ == tcl) return;
+  // bucket (w, b-1) has weight b in window w; top window: slot k holds a copy
+  // of bucket (k mod ntop) + 1
+  std::vector<uint32_t> wt(NT), win(NT);
+  const size_t ntop = NB >> tcl;
+  for (size_t k = 0; k < NT; ++k) {
+    const size_t w = k / NB, b = k % NB;
+    wt[k] = (uint32_t)((w == (size_t)W - 1 ? b % ntop : b) + 1);
+    win[k] = (uint32_t)w;
   }
-  red_.launch(s, buckets_.p);
+  red_.plan(wt, win, W);
+  red_W_ = W;
+  red_tcl_ = tcl;
+}
+
+template <int G>
+void Pippenger<G>::back(hipStream_t s, int nbits, hfp::Jac<HF> *out) {
+  const int c = c_;
+  accumulate(s, nbits, fs_[0], buckets_[0]);
+  if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[3], s));
+  plan_reduction(nbits);
+  red_.launch(s, buckets_[0].p);
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[4], s));
-  std::vector<hfp::Jac<HF>> T = red_.read_windows(s);
+  *out = red_.read_total(s, c);
   if (profile_) MSM_HIP_CHECK(hipEventRecord(ev_[5], s));
-  MSM_HIP_CHECK(hipStreamSynchronize(s));
-  *out = horner(T, c);
   if (profile_) {
     float ms;
+    MSM_HIP_CHECK(hipEventSynchronize(ev_[5]));
     MSM_HIP_CHECK(hipEventElapsedTime(&ms, ev_[0], ev_[1]));
     times_.digits = ms;
     MSM_HIP_CHECK(hipEventElapsedTime(&ms, ev_[1], ev_[2]));
@@ -238,8 +260,95 @@ void Pippenger<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, i
     *out = hfp::Jac<HF>{hfp::fzero(HF()), hfp::fzero(HF()), hfp::fzero(HF())};
     return;
   }
-  front(s, d_scalars, stride, nbits, nullptr);
+  front(s, d_scalars, stride, nbits, nullptr, fs_[0]);
   back(s, nbits, out);
+}
+
+template <int G>
+void Pippenger<G>::run_batch(hipStream_t s, const uint8_t *d_scalars, size_t stride, size_t set_stride, size_t count,
+                             int nbits, hfp::Jac<HF> *outs) {
+  typedef typename FieldOf<G>::F F;
+  DeviceGuard g(dev_);
+  if (nbits < 1 || nbits > 256) throw std::runtime_error("nbits must be in [1,256]");
+  if (count == 0) return;
+  if (n_ == 0) {
+    for (size_t k = 0; k < count; ++k) outs[k] = hfp::Jac<HF>{hfp::fzero(HF()), hfp::fzero(HF()), hfp::fzero(HF())};
+    return;
+  }
+  const int W = (nbits + 1 + c_ - 1) / c_;
+  const size_t NT = (size_t)W << (c_ - 1);
+  plan_reduction(nbits);
+  if (!fstream_) {
+    int least = 0, greatest = 0;
+    MSM_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    MSM_HIP_CHECK(hipStreamCreateWithPriority(&fstream_, hipStreamNonBlocking, greatest));
+    MSM_HIP_CHECK(hipStreamCreateWithFlags(&lane1_, hipStreamNonBlocking));
+    MSM_HIP_CHECK(hipStreamCreateWithFlags(&tstream_, hipStreamNonBlocking));
+  }
+  // groups of R <= kGroup MSMs share one reduction tail (WeightedReducer batch groups)
+  const size_t ngroups = (count + kGroup - 1) / kGroup, R = (count + ngroups - 1) / ngroups;
+  const size_t ob = red_.out_bytes();
+  if (host_out_bytes_ < count * ob) {
+    if (host_out_) (void)hipHostFree(host_out_);
+    host_out_ = nullptr;
+    host_out_bytes_ = 0;
+    const size_t bytes = std::max<size_t>(count, 64) * ob;
+    MSM_HIP_CHECK(hipHostMalloc(&host_out_, bytes, hipHostMallocDefault));
+    host_out_bytes_ = bytes;
+  }
+  // every buffer the pipeline touches exists before its first launch (an
+  // allocation inside the issue loop would synchronise the device)
+  for (DevBuf &b : buckets_) b.ensure(NT * sizeof(Xyzz<F>));
+  for (int t = 0; t < kRedSets; ++t) red_.ensure_group(t, kGroup);
+  for (int f = 0; f < kFronts; ++f)
+    if (fs_[f].sorted.bytes < (size_t)W * n_ * 4 + 64) front(s, d_scalars, stride, nbits, nullptr, fs_[f]);
+  MSM_HIP_CHECK(hipStreamSynchronize(s));
+  while (bev_.size() < 3 * count + ngroups + 1) {
+    hipEvent_t e;
+    MSM_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    bev_.push_back(e);
+  }
+  hipEvent_t *evf = bev_.data() + 1, *eva = evf + count, *evh = eva + count, *evt = evh + count;
+  MSM_HIP_CHECK(hipEventRecord(bev_[0], s));
+  for (hipStream_t q : {fstream_, lane1_, tstream_}) MSM_HIP_CHECK(hipStreamWaitEvent(q, bev_[0], 0));
+  auto front_k = [&](size_t k) {
+    if (k >= count) return;
+    if (k >= (size_t)kFronts) MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, eva[k - kFronts], 0));  // front set free
+    front(fstream_, d_scalars + k * set_stride, stride, nbits, nullptr, fs_[k % kFronts]);
+    MSM_HIP_CHECK(hipEventRecord(evf[k], fstream_));
+  };
+  hipStream_t lane[2] = {s, lane1_};
+  for (size_t k = 0; k + 1 < (size_t)kFronts; ++k) front_k(k);
+  for (size_t k = 0; k < count; ++k) {
+    front_k(k + kFronts - 1);
+    hipStream_t L = lane[k & 1];
+    const size_t q = k / R;
+    const int slot = (int)(k % R), gset = (int)(q % kRedSets);
+    MSM_HIP_CHECK(hipStreamWaitEvent(L, evf[k], 0));
+    if (q >= (size_t)kRedSets && slot < 2)  // reducer set q % kRedSets free again (tail q - kRedSets)
+      MSM_HIP_CHECK(hipStreamWaitEvent(L, evt[q - kRedSets], 0));
+    accumulate(L, nbits, fs_[k % kFronts], buckets_[k & 1]);  // bucket set k % 2: lane k % 2 only, in order
+    MSM_HIP_CHECK(hipEventRecord(eva[k], L));
+    red_.launch_head_slot(L, buckets_[k & 1].p, gset, slot);
+    MSM_HIP_CHECK(hipEventRecord(evh[k], L));
+    if ((size_t)slot + 1 == R || k + 1 == count) {
+      for (int d = 0; d < 2 && d <= slot; ++d) MSM_HIP_CHECK(hipStreamWaitEvent(tstream_, evh[k - d], 0));
+      red_.launch_tail_group(tstream_, gset, slot + 1);
+      red_.copy_out_group(tstream_, gset, slot + 1, (uint8_t *)host_out_ + (k - slot) * ob);
+      MSM_HIP_CHECK(hipEventRecord(evt[q], tstream_));
+    }
+  }
+  // the host Horner of group q overlaps the GPU work of later groups
+  for (size_t q = 0; q * R < count; ++q) {
+    MSM_HIP_CHECK(hipEventSynchronize(evt[q]));
+    for (size_t k = q * R; k < std::min(count, (q + 1) * R); ++k)
+      outs[k] = red_.combine_windows((const uint8_t *)host_out_ + k * ob, c_);
+  }
+  // the caller's stream observes completion of every stream of the batch
+  for (hipStream_t q : {fstream_, lane1_, tstream_}) {
+    MSM_HIP_CHECK(hipEventRecord(bev_[0], q));
+    MSM_HIP_CHECK(hipStreamWaitEvent(s, bev_[0], 0));
+  }
 }
 
 // The blst drop-in (abi.cpp blst_p{1,2}s_mult_pippenger / _tile_pippenger):
@@ -283,9 +392,9 @@ void Pippenger<G>::run_host(hipStream_t s, const void *pts_blst, size_t n, const
                        tile->bit0, tile->wbits, tile->cbits, mag, neg);
     MSM_HIP_CHECK(hipGetLastError());
     nbits = tile->cbits + 1;
-    front(s, reinterpret_cast<const uint8_t *>(mag), 4, nbits, neg);
+    front(s, reinterpret_cast<const uint8_t *>(mag), 4, nbits, neg, fs_[0]);
   } else {
-    front(s, scal_.as<uint8_t>(), stride, nbits, nullptr);
+    front(s, scal_.as<uint8_t>(), stride, nbits, nullptr, fs_[0]);
   }
   const size_t raw = n * 96 * G;
   tmp_.ensure(raw);

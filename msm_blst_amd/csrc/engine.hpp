@@ -183,7 +183,7 @@ template <int G>
 class WeightedReducer {
  public:
   typedef typename HostField<G>::F HF;
-  static constexpr int NSETS = 2;  // buffer sets, allocated on first use (Ches batch: one per bucket set)
+  static constexpr int NSETS = 4;  // buffer sets, allocated on first use (batch reduction groups rotate over them)
   // win[i] in [0, nwin): the window of bucket i (empty = all in window 0)
   void plan(const std::vector<uint32_t> &w, const std::vector<uint32_t> &win, int nwin);
   void plan(const std::vector<uint32_t> &w) { plan(w, {}, 1); }
@@ -197,8 +197,14 @@ class WeightedReducer {
   size_t out_bytes() const { return (size_t)2 * nwin_ * 144 * G; }
   void copy_out(hipStream_t s, int set, void *host);               // async D2H of out_bytes()
   std::vector<hfp::Jac<HF>> combine(const void *host) const;        // per-window sums
+  // sum_w 2^(c w) T_w of a copied-out result in ONE Horner pass over the 2 nwin
+  // terms L_w (exponent c w) and H_w (c w + s): (nwin - 1) c + s doublings
+  // instead of nwin s + (nwin - 1) c (combine, then horner over the windows)
+  hfp::Jac<HF> combine_windows(const void *host, int c) const;
   std::vector<hfp::Jac<HF>> read_windows(hipStream_t s);            // set 0, waits
   hfp::Jac<HF> read(hipStream_t s) { return read_windows(s)[0]; }
+  // set 0's sum_w 2^(c w) T_w (after launch_tail), waits
+  hfp::Jac<HF> read_total(hipStream_t s, int c);
   size_t size() const { return bsize_; }
 
   void ensure_set(int set);  // allocate buffer set `set` for the current plan
@@ -234,6 +240,17 @@ class WeightedReducer {
   DevBuf bfin_;
 };
 
+// digit/sort outputs of one MSM (entries sorted by bucket + schedule); the
+// CHES and plain Pippenger batches rotate three of them (front k + 2 beside
+// accumulation k)
+struct ChesFrontSet {
+  DevBuf keys, vals, sorted, counts, offsets, order;
+  BucketSort sort;
+  size_t device_bytes() const {
+    return keys.bytes + vals.bytes + sorted.bytes + counts.bytes + offsets.bytes + order.bytes + sort.device_bytes();
+  }
+};
+
 // one blst window tile (ref multi_scalar.c:383-419): Booth digit over bits
 // [bit0 - 1, bit0 + wbits), cbits = wbits (+ 1 for the top, partial window)
 struct TileSpec {
@@ -256,6 +273,14 @@ class Pippenger {
   // tile: one blst window tile instead of the whole MSM (blst_p{1,2}s_tile_pippenger)
   void run_host(hipStream_t s, const void *points_blst, size_t n, const uint8_t *scalars, size_t stride, int nbits,
                 hfp::Jac<HF> *out, const TileSpec *tile = nullptr);
+  // `count` MSMs over the resident points, scalar set k at d_scalars + k
+  // set_stride (device memory), pipelined: front k + 2 (digits + sort) on a
+  // front stream beside accumulation k; accumulations alternate between two
+  // lane streams (each followed by its level 0); the reduction tails of groups
+  // of <= 8 MSMs on a tail stream; the host Horner of group q overlaps the GPU
+  // work of later groups.  Results equal `count` run() calls.
+  void run_batch(hipStream_t s, const uint8_t *d_scalars, size_t stride, size_t set_stride, size_t count, int nbits,
+                 hfp::Jac<HF> *outs);
   size_t npoints() const { return n_; }
   void set_profiling(bool on) { profile_ = on; }
   const PhaseTimes &times() const { return times_; }
@@ -270,14 +295,22 @@ class Pippenger {
   size_t n_ = 0;
   bool profile_ = false;
   PhaseTimes times_;
-  DevBuf pts_, keys_, vals_, counts_, offsets_, sorted_, order_, buckets_, tmp_, scal_;
+  static constexpr int kFronts = 5, kGroup = 8, kRedSets = 4;
+  ChesFrontSet fs_[kFronts];  // digit/sort outputs: fs_[0] for run(), all of them for run_batch()
+  DevBuf pts_, buckets_[2], tmp_, scal_;
   std::unique_ptr<HostStager> stage_;  // run_host: uploads from the caller's pageable memory
   hipStream_t up_ = nullptr;  // run_host: point upload stream
   hipEvent_t ev_up_ = nullptr, ev_s_ = nullptr;
-  // digits + sort; neg: optional per-point sign flips (tiles)
-  void front(hipStream_t s, const uint8_t *d_scalars, size_t stride, int nbits, const uint8_t *neg);
-  void back(hipStream_t s, int nbits, hfp::Jac<HF> *out);  // accumulate + reduce + read-back
-  BucketSort sort_;
+  // run_batch: front stream, second accumulation lane, tail stream; events; read-back slots
+  hipStream_t fstream_ = nullptr, lane1_ = nullptr, tstream_ = nullptr;
+  std::vector<hipEvent_t> bev_;
+  void *host_out_ = nullptr;
+  size_t host_out_bytes_ = 0;
+  // digits + sort into f; neg: optional per-point sign flips (tiles)
+  void front(hipStream_t s, const uint8_t *d_scalars, size_t stride, int nbits, const uint8_t *neg, ChesFrontSet &f);
+  void accumulate(hipStream_t s, int nbits, ChesFrontSet &f, DevBuf &buckets);
+  void plan_reduction(int nbits);  // reducer plan for this window layout (built once)
+  void back(hipStream_t s, int nbits, hfp::Jac<HF> *out);  // accumulate + reduce + read-back (fs_[0])
   WeightedReducer<G> red_;
   int red_W_ = 0, red_tcl_ = -1;  // window count / top copies the reducer plan was built for
   // log2 of the top window's bucket copies (k_digits): 2^topbits digit values
@@ -290,11 +323,6 @@ class Pippenger {
   std::vector<hipEvent_t> ev_;
 };
 
-// digit/sort outputs of one CHES MSM (entries sorted by bucket + schedule)
-struct ChesFrontSet {
-  DevBuf keys, vals, sorted, counts, offsets, order;
-  BucketSort sort;
-};
 
 template <int G>
 class Ches {
@@ -362,8 +390,10 @@ class Ches {
   static constexpr int kGroup = 8;       // batch: MSMs per reduction group (WeightedReducer::launch_tail_group)
   static constexpr int kFrontGroup = 8;  // batch: largest front group (ramping up 1, 1, 2, 4, 8)
   static constexpr int kFrontGroupDefault = 1;
-  static constexpr int kFronts = 3;  // front k+1 may start when accumulation k-2 ends (slack for the copies)
-  ChesFrontSet fs_[kFronts];
+  // front k+1 may start when accumulation k-2 ends (slack for the copies); the
+  // lane schedule of small MSMs rotates kFrontsMax sets (fronts further ahead)
+  static constexpr int kFronts = 3, kFrontsMax = 5;
+  ChesFrontSet fs_[kFrontsMax];
   // host scalar sets of a batch: two groups of kFrontGroup device slots, copied on
   // their own stream (cstream_) ahead of the group's front
   DevBuf scal_;
@@ -459,6 +489,16 @@ class Wbits {
 template <int G>
 void entry_msm(void *ret_jac, const void *pts_blst, size_t npts, const uint32_t *keys, const uint32_t *vals,
                size_t ne, size_t nb, const uint32_t *weights, void *buckets_out);
+// The same for entries named by per-entry point pointers (the blst-level CHES /
+// BGMW95 tiles: entry t's point is *points[t], ref multi_scalar.c:421-547):
+// fill(ctx, t0, t1, keys, vals) writes the keys / vals of entries [t0, t1)
+// (called concurrently on disjoint ranges by the host worker pool).  Keys,
+// vals and the gathered point rows are staged through page-locked memory in
+// chunks, the host gather of chunk c + 1 overlapping the DMA of chunk c.
+typedef void (*EntryFill)(void *ctx, size_t t0, size_t t1, uint32_t *keys, uint32_t *vals);
+template <int G>
+void entry_msm_ptrs(void *ret, const void *const *points, size_t ne, EntryFill fill, void *fill_ctx, size_t nb,
+                    const uint32_t *weights, void *buckets_out);
 // sum_i weights[i] * buckets[i] for nb blst xyzz buckets in host memory
 template <int G>
 void weighted_bucket_sum(void *ret_jac, const void *buckets_blst, size_t nb, const uint32_t *weights);

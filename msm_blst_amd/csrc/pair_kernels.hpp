@@ -43,6 +43,110 @@ __device__ __forceinline__ void st_xyzz2l(Xyzz<Fp2> *p, const Xyzz<Fp2L> &a, int
   st_comp(&p->zz, a.zz.c, comp);
 }
 
+// 1 / (a0 + a1 i) = (a0 - a1 i) / (a0^2 + a1^2) on a lane pair: both lanes form
+// the norm a0^2 + a1^2 (own square + partner's square) and invert it (the same
+// instructions on both lanes), then scale their own (negated on odd lanes)
+// component.  a in S.
+__device__ __forceinline__ void f_inv(Fp2L &r, const Fp2L &a) {
+  Fp own = a.c, sq, psq, d, neg, x;
+  fp_norm(own);
+  fp_sqr(sq, own);
+  pair_swap(psq, sq);
+  fp_add(d, sq, psq);  // < 4p lazy
+  fp_inv(d, d);
+  fp_neg<4>(neg, own);
+  pair_sel(x, pair_odd(), neg, own);
+  fp_mul(r.c, x, d);
+}
+__device__ __forceinline__ void f_csub(Fp2L &a) { fp_csub_p(a.c); }
+
+// k_ches_table (ches_kernels.hpp) for G2 on lane pairs: lanes 2t, 2t + 1 build
+// the rows of base point i0 + t, one Fp2 component each.  The one-lane G2
+// table kernel needed 256 VGPRs + 256 AGPRs + 1.5 KB/lane of scratch (and a
+// call); its device results changed with a source-equivalent reordering of
+// xyzz_dbl (tests/test_gpu_table_rows.py).  Here a lane holds one
+// component: the register use of the G1 kernel, no spills.
+template <int M>
+static __global__ void __launch_bounds__(128)
+    k_ches_table2p(const Aff<Fp2> *__restrict__ P, size_t i0, size_t cnt, int q_exp, int h,
+                   Xyzz<Fp2> *__restrict__ scratch, Fp2 *__restrict__ pref, AffP<Fp2> *__restrict__ T) {
+  const size_t tt = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tt >= 2 * cnt) return;  // whole pairs only
+  const int comp = (int)(tt & 1);
+  const size_t t = tt >> 1, i = i0 + t;
+  static_assert(M == 1 || M == 3, "M");
+  const int K = M * h;
+  Aff<Fp2L> p;
+  ld_point2l(p, &P[i], comp);
+  AffP<Fp2> *out = T + (size_t)K * i;
+  static_assert(sizeof(AffP<Fp2>) == 256, "one G2 row per 256 B");
+  if (f_is_zero_exact(p.x) && f_is_zero_exact(p.y)) {  // infinity: every multiple is infinity (uniform per pair)
+    Fp z;
+    fp_zero(z);
+    for (int k = 0; k < K; ++k) {
+      Aff<Fp2> *o = reinterpret_cast<Aff<Fp2> *>(out + k);
+      st_comp(&o->x, z, comp);
+      st_comp(&o->y, z, comp);
+    }
+    return;
+  }
+  Xyzz<Fp2L> Q;
+  xyzz_from_aff(Q, p, false);
+  for (int j = 0; j < h; ++j) {
+    st_xyzz2l(&scratch[(size_t)(M * j) * cnt + t], Q, comp);
+    if (M == 3) {  // 2 Q, then 3 Q = 2 Q + Q in place (one point fewer live)
+      Xyzz<Fp2L> R;
+      xyzz_dbl(R, Q);
+      st_xyzz2l(&scratch[(size_t)(3 * j + 1) * cnt + t], R, comp);
+      xyzz_add(R, Q);
+      st_xyzz2l(&scratch[(size_t)(3 * j + 2) * cnt + t], R, comp);
+    }
+    if (j + 1 < h)
+      for (int e = 0; e < q_exp; ++e) {
+        Xyzz<Fp2L> tmp = Q;
+        xyzz_dbl(Q, tmp);
+      }
+  }
+  // Montgomery batch inversion of u_k = ZZ_k ZZZ_k (1/ZZ = ZZZ/u, 1/ZZZ = ZZ/u)
+  Fp2L c;
+  f_one(c);
+  for (int k = 0; k < K; ++k) {
+    Xyzz<Fp2L> a;
+    ld_xyzz2l(a, &scratch[(size_t)k * cnt + t], comp);
+    Fp2L u;
+    f_mul(u, a.zz, a.zzz);
+    f_mul(c, c, u);
+    st_comp(&pref[(size_t)k * cnt + t], c.c, comp);
+  }
+  Fp2L inv;
+  f_inv(inv, c);
+  for (int k = K - 1; k >= 0; --k) {
+    Xyzz<Fp2L> a;
+    ld_xyzz2l(a, &scratch[(size_t)k * cnt + t], comp);
+    Fp2L ik;
+    if (k > 0) {
+      Fp2L pk;
+      ld_comp(pk.c, &pref[(size_t)(k - 1) * cnt + t], comp);
+      f_mul(ik, inv, pk);
+      Fp2L u;
+      f_mul(u, a.zz, a.zzz);
+      f_mul(inv, inv, u);
+    } else {
+      ik = inv;
+    }
+    Fp2L izz, izzz, x, y;
+    f_mul(izz, ik, a.zzz);
+    f_mul(izzz, ik, a.zz);
+    f_mul(x, a.x, izz);
+    f_mul(y, a.y, izzz);
+    f_csub(x);
+    f_csub(y);
+    Aff<Fp2> *o = reinterpret_cast<Aff<Fp2> *>(out + k);
+    st_comp(&o->x, x.c, comp);
+    st_comp(&o->y, y.c, comp);
+  }
+}
+
 // k_accumulate (kernels.hpp) for G2 with two lanes per bucket
 template <class PT>
 __global__ void __launch_bounds__(256)

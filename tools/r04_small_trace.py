@@ -51,6 +51,29 @@ def plain(lg, c):
     time.sleep(0.05)
 
 
+def plain_batch(lg, c):
+    n = 1 << lg
+    pts = m.fixed_points(1, n)
+    d = dev_sets(n, K)
+    ctx = m.MSMContext(1, 0, c)
+    ctx.set_points(pts, n)
+    ctx.mult_batch(d.data_ptr(), K, 255, on_device=True)
+    ref = [m.compress(1, ctx.mult(d.data_ptr() + i * 32 * n, 255, on_device=True)) for i in range(3)]
+    time.sleep(0.05)
+    best = 1e9
+    for _ in range(3):
+        torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        got = ctx.mult_batch(d.data_ptr(), K, 255, on_device=True)
+        torch.cuda.synchronize(dev)
+        best = min(best, (time.perf_counter() - t) / K * 1e3)
+    ok = [m.compress(1, j) for j in got[:3]] == ref
+    print(f"plain batch 2^{lg} c={c}: {best:.3f} ms/MSM = {n / best / 1e3:.1f} M pairs/s (K={K}, equals sync: {ok})",
+          flush=True)
+    ctx.close()
+    time.sleep(0.05)
+
+
 def ches(lg, beta=0):
     n = 1 << lg
     pts = m.fixed_points(1, n)
@@ -85,6 +108,9 @@ CASES = {
     "p10": lambda: plain(10, 10),
     "p16": lambda: plain(16, 14),
     "p16c13": lambda: plain(16, 13),
+    "pb16": lambda: plain_batch(16, 14),
+    "pb16c13": lambda: plain_batch(16, 13),
+    "pb16c12": lambda: plain_batch(16, 12),
     "c17": lambda: ches(17),
     "c17b": lambda: ches(17, 1),
     "c18": lambda: ches(18),
