@@ -768,12 +768,13 @@ void Ches<G>::digits_sort(hipStream_t s, const uint8_t *d_scalars, size_t stride
 }
 
 template <int G>
-void Ches<G>::accumulate(hipStream_t s, int set, int r, int bset) {
+void Ches<G>::accumulate(hipStream_t s, int set, int r, int bset, const void *table) {
   typedef typename FieldOf<G>::F F;
   const size_t NB = bucket_count();
   ChesFrontSet &f = fs_[set];
   buckets_[bset].ensure(NB * sizeof(Xyzz<F>));
-  launch_accumulate<G>(s, f.sort.sched(f.order.as<uint32_t>(), f.sorted.as<uint32_t>(), r, NB), table_.as<AffP<F>>(),
+  launch_accumulate<G>(s, f.sort.sched(f.order.as<uint32_t>(), f.sorted.as<uint32_t>(), r, NB),
+                       table ? static_cast<const AffP<F> *>(table) : table_.as<AffP<F>>(),
                        buckets_[bset].as<Xyzz<F>>(), NB);
   MSM_HIP_CHECK(hipGetLastError());
 }
@@ -815,15 +816,24 @@ void Ches<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, hfp::J
 }
 
 template <int G>
-void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, size_t set_stride, size_t count,
-                        hfp::Jac<HF> *outs, bool scalars_on_host) {
+void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, size_t set_stride, size_t nsets,
+                       size_t nseg, const void *const *tables, hfp::Jac<HF> *outs, bool scalars_on_host) {
   DeviceGuard g(dev_);
   if (stride < 32) throw std::runtime_error("CHES scalars must be 32-byte strings");
+  if (nseg < 1) throw std::runtime_error("run_jobs: no segments");
+  // jobs k = set (k / nseg), segment (k % nseg); every loop below runs over jobs
+  const size_t count = nsets * nseg;
   if (count == 0) return;
   if (n_ == 0) {
     std::memset(outs, 0, sizeof(*outs) * count);
     return;
   }
+  auto job_scalars = [&](size_t k) { return scalars + (k / nseg) * set_stride + (k % nseg) * n_ * stride; };
+  auto job_table = [&](size_t k) { return tables[k % nseg]; };
+  // a front group of several jobs reads their scalars with one stride: the
+  // segments' slices are n strings apart, so groups > 1 need packed sets
+  const size_t jstride = nseg == 1 ? set_stride : n_ * stride;
+  const bool packed = nseg == 1 || set_stride == nseg * n_ * stride;
   if (!fstream_) {
     // fronts at the greatest priority: their short memory-bound kernels take the
     // first CU slots an accumulation releases (the next accumulation waits for
@@ -858,10 +868,11 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
     host_out_bytes_ = bytes;
   }
   // (group size cap: kFrontGroupDefault, or MSM_FRONT_GROUP=<1..8>; engine.hpp)
-  static const size_t fg_max = [] {
+  static const size_t fg_env = [] {
     const char *e = getenv("MSM_FRONT_GROUP");
     return (size_t)std::min(kFrontGroup, std::max(1, e ? atoi(e) : kFrontGroupDefault));
   }();
+  const size_t fg_max = packed ? fg_env : 1;
   // front groups of 1, 1, 2, 4, then fg_max MSMs: the first accumulation
   // starts after one front, and each group's host sets (copied while the earlier
   // groups accumulate: a set copies in ~0.6 ms, an MSM accumulates in ~2.3) are
@@ -901,7 +912,18 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
   }();
   // (every group's copies are enqueued before its front: nsg >= nfr - 1)
   const size_t nsg = std::max<size_t>(nsg_env ? nsg_env : fg_max == 1 ? 4 : 2, (size_t)nfr - 1);
-  if (scalars_on_host || unsized) scal_.ensure(std::max<size_t>(nsg, 2) * fg_max * sslot + 16);
+  if (scalars_on_host || unsized) {
+    const size_t before = scal_.bytes;
+    scal_.ensure(std::max<size_t>(nsg, 2) * fg_max * sslot + 16);
+    static const bool touch_env = [] {  // A/B knob: write every new slot once before the first batch uses it
+      const char *e = getenv("MSM_TOUCH_SLOTS");
+      return e && atoi(e) != 0;
+    }();
+    if (touch_env && scal_.bytes != before) {
+      MSM_HIP_CHECK(hipMemsetAsync(scal_.p, 0, scal_.bytes, s));
+      MSM_HIP_CHECK(hipStreamSynchronize(s));
+    }
+  }
   for (int f = 0; f < nfr; ++f)
     if (fs_[f].sorted.bytes < n * (size_t)p_.h * fg_max * 4) {
       MSM_HIP_CHECK(hipMemsetAsync(scal_.p, 0, fg_max * sslot, s));
@@ -968,8 +990,8 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
     if (!scalars_on_host || zero_copy || g >= nfg) return;
     if (g >= nsg) MSM_HIP_CHECK(hipStreamWaitEvent(cstream_, evf[g - nsg], 0));  // slots consumed by front g - nsg
     for (size_t k = fgb[g]; k < fgb[g + 1]; ++k)
-      MSM_HIP_CHECK(hipMemcpyAsync(slots(g) + (k - fgb[g]) * sslot, scalars + k * set_stride, sslot,
-                                   hipMemcpyHostToDevice, cstream_));
+      MSM_HIP_CHECK(hipMemcpyAsync(slots(g) + (k - fgb[g]) * sslot, job_scalars(k), sslot, hipMemcpyHostToDevice,
+                                   cstream_));
     MSM_HIP_CHECK(hipEventRecord(evc[g], cstream_));
   };
   auto front_group = [&](size_t g) {
@@ -982,8 +1004,8 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
       for (size_t d = 1; d < (size_t)nl && last >= d && last - d >= fgb[g - nfr]; ++d)  // its other lanes
         MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, eva[last - d], 0));
     }
-    const uint8_t *src = copied ? slots(g) : scalars + fgb[g] * set_stride;
-    digits_sort(fstream_, src, stride, copied ? sslot : set_stride, (int)(fgb[g + 1] - fgb[g]), (int)(g % nfr));
+    const uint8_t *src = copied ? slots(g) : job_scalars(fgb[g]);
+    digits_sort(fstream_, src, stride, copied ? sslot : jstride, (int)(fgb[g + 1] - fgb[g]), (int)(g % nfr));
     MSM_HIP_CHECK(hipEventRecord(evf[g], fstream_));
   };
   for (size_t g = 0; g < nsg; ++g) copy_group(g);
@@ -1028,7 +1050,7 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
         if (q >= (size_t)nred && slot < nl)  // reducer set q % nred free again
           MSM_HIP_CHECK(hipStreamWaitEvent(L, evt[q - nred], 0));
         if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k], L));
-        accumulate(L, (int)(g % nfr), (int)(k - fgb[g]), bset);
+        accumulate(L, (int)(g % nfr), (int)(k - fgb[g]), bset, job_table(k));
         if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k + 1], L));
         MSM_HIP_CHECK(hipEventRecord(eva[k], L));
         red_.launch_head_slot(L, buckets_[bset].p, gset, slot);
@@ -1052,7 +1074,7 @@ void Ches<G>::run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, si
       if (k >= (size_t)kBSets) MSM_HIP_CHECK(hipStreamWaitEvent(s, evh[k - kBSets], 0));  // bucket set free again
       if (l0_first && k >= 1) MSM_HIP_CHECK(hipStreamWaitEvent(s, evh[k - 1], 0));
       if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k], s));
-      accumulate(s, (int)(g % nfr), (int)(k - fgb[g]), bset);
+      accumulate(s, (int)(g % nfr), (int)(k - fgb[g]), bset, job_table(k));
       if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k + 1], s));
       MSM_HIP_CHECK(hipEventRecord(eva[k], s));
       MSM_HIP_CHECK(hipStreamWaitEvent(ts, eva[k], 0));

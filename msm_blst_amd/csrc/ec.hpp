@@ -63,9 +63,13 @@ MSM_FN void xyzz_dbl(Xyzz<F> &r, const Xyzz<F> &a) {
     r = a;
     return;
   }
-#if MSM_DBL_LEAN
-  // (study build, tools/r04_g2table.sh) ordered so that each input coordinate
-  // dies at its last use: ZZ3, ZZZ3 first
+  // ordered so that each input coordinate dies at its last use (ZZ3, ZZZ3
+  // first; r may alias a).  Round 3 reverted this order because compiled into
+  // the one-lane G2 table kernel (256 VGPR + 256 AGPR + 1.5 KB scratch) it gave
+  // wrong rows on the device only: 2Q right, then Q itself corrupted across
+  // the call (3Q and every later row wrong; tests/test_gpu_table_rows.py).  The
+  // lane-pair table kernel has no spills and builds correct rows with it
+  // (DESIGN 11).
   F U, V, W, S, M, t, X3;
   f_add(U, a.y, a.y);      // < 4p lazy
   f_sqr(V, U);             // S
@@ -83,26 +87,6 @@ MSM_FN void xyzz_dbl(Xyzz<F> &r, const Xyzz<F> &a) {
   f_sub16(t, S, X3);       // < 18p
   f_mul_sub(r.y, t, M, W, a.y);  // Y3 = M (S - X3) - W Y   S (one reduction)
   r.x = X3;
-#else
-  F U, V, W, S, M, t, X3, Y3;
-  f_add(U, a.y, a.y);      // < 4p lazy
-  f_sqr(V, U);             // S
-  f_mul(W, V, U);          // S
-  f_mul(S, a.x, V);        // S
-  f_sqr(M, a.x);           // S
-  f_mul3(M, M);            // < 6p lazy
-  f_sqr(X3, M);            // S
-  F z;
-  f_zero(z);
-  f_sub_2x(X3, X3, z, S);  // M^2 + 8p - 2S   < 10p
-  f_norm(X3);              // X
-  f_sub16(t, S, X3);       // < 18p
-  f_mul_sub(Y3, t, M, W, a.y);  // M (S - X3) - W Y   S (one reduction)
-  f_mul(r.zz, V, a.zz);
-  f_mul(r.zzz, W, a.zzz);
-  r.y = Y3;
-  r.x = X3;
-#endif
 }
 
 // acc += (neg ? -P : P); P affine, canonical, not infinity (callers skip the

@@ -352,7 +352,18 @@ class Ches {
   // accumulations, MSM k's reduction on a second stream beside MSM k+1's
   // accumulation.
   void run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, size_t set_stride, size_t count,
-                 hfp::Jac<HF> *outs, bool scalars_on_host = false);
+                 hfp::Jac<HF> *outs, bool scalars_on_host = false) {
+    const void *t = table_.p;
+    run_jobs(s, scalars, stride, set_stride, count, 1, &t, outs, scalars_on_host);
+  }
+  // The batch over nseg point segments of n_ points each, one pipeline: segment
+  // d's table is tables[d] (engines of the same parameters and n on this
+  // device, e.g. the shards of a multi-shard context that share a GPU), its
+  // scalars the d-th n-string slice of every set.  outs: count * nseg partial
+  // Jacobians, job k nseg + d = (set k, segment d).
+  void run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, size_t set_stride, size_t count, size_t nseg,
+                const void *const *tables, hfp::Jac<HF> *outs, bool scalars_on_host);
+  const void *table_ptr() const { return table_.p; }
   size_t npoints() const { return n_; }
   const ChesParams &params() const { return p_; }
   size_t bucket_count() const { return B_.size() + (size_t)(copies_ - 1) * small_; }
@@ -409,7 +420,8 @@ class Ches {
   // digits + sort of nsets scalar sets (set_stride bytes apart) into front set `set`
   void digits_sort(hipStream_t s, const uint8_t *d_scalars, size_t stride, size_t set_stride, int nsets, int set);
   // accumulation of scalar set r of front set `set` into bucket set bset
-  void accumulate(hipStream_t s, int set, int r, int bset);
+  // (table: the table_ of this engine, or of a segment's engine in run_jobs)
+  void accumulate(hipStream_t s, int set, int r, int bset, const void *table = nullptr);
 };
 
 // BGMW95 fixed-base variant (ref main_p1.cpp:94-122, 294-398;

@@ -168,6 +168,22 @@ class ChesMulti {
                  hfp::Jac<HF> *outs, bool on_host) {
     if (shards_.size() == 1) return shards_[0].eng->run_batch(s, scalars, stride, set_stride, count, outs, on_host);
     if (!on_host) throw std::runtime_error("multi-device mult_batch takes host scalars");
+    if (one_device_pipeline()) {
+      // every shard on one device: ONE pipeline over the count x D jobs (set k,
+      // shard d) with each shard's table (Ches::run_jobs), instead of D engines
+      // with five streams each competing for the device's four hardware queues
+      const size_t D = shards_.size();
+      std::vector<const void *> tabs(D);
+      for (size_t g = 0; g < D; ++g) tabs[g] = shards_[g].eng->table_ptr();
+      std::vector<hfp::Jac<HF>> part(count * D);
+      Shard &sh = shards_[0];
+      DeviceGuard g(sh.device);
+      sh.eng->run_jobs(sh.stream, scalars, stride, set_stride, count, D, tabs.data(), part.data(), true);
+      MSM_HIP_CHECK(hipStreamSynchronize(sh.stream));
+      for (size_t k = 0; k < count; ++k)
+        outs[k] = fold(std::vector<hfp::Jac<HF>>(part.begin() + k * D, part.begin() + (k + 1) * D));
+      return;
+    }
     std::vector<std::vector<hfp::Jac<HF>>> part(shards_.size(), std::vector<hfp::Jac<HF>>(count));
     each([&](Shard &sh) {
       std::vector<hfp::Jac<HF>> &r = part[&sh - shards_.data()];
@@ -195,6 +211,18 @@ class ChesMulti {
   std::vector<Shard> shards_;
   size_t n_ = 0;
 
+  // all shards on one device with equal point counts (MSM_MULTI_PIPELINE=0: one
+  // engine per shard, concurrently, as on separate devices)
+  bool one_device_pipeline() const {
+    static const bool env = [] {
+      const char *e = getenv("MSM_MULTI_PIPELINE");
+      return !e || atoi(e) != 0;
+    }();
+    if (!env || shards_.size() < 2 || shards_[0].n == 0) return false;
+    for (const Shard &sh : shards_)
+      if (sh.device != shards_[0].device || sh.n != shards_[0].n) return false;
+    return true;
+  }
   void split(size_t n) {
     const size_t S = shards_.size(), base = n / S, rem = n % S;
     size_t at = 0;

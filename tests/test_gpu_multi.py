@@ -30,7 +30,34 @@ def test_configs3_2e21_over_8_shards(m, golden):
     ctx.build_table(m.fixed_points(1, n), n)
     sc = m.gen_scalars(n, 1)
     assert m.compress(1, ctx.mult(sc)).hex() == _golden(golden, 1, n)
+    # the batch: all 8 shards share device 0, so it runs as ONE pipeline over
+    # (set, shard) jobs (Ches::run_jobs), each job reading its shard's table
+    sets = bytes(sc) + bytes(m.gen_scalars(n, 7))
+    got = ctx.mult_batch(sets, 2)
+    assert m.compress(1, got[0]).hex() == _golden(golden, 1, n)
+    assert m.compress(1, got[1]) == m.compress(1, ctx.mult(sets[32 * n:]))
     ctx.close()
+
+
+@pytest.mark.parametrize("group,shards,count", [(1, 4, 6), (2, 2, 3)])
+def test_one_device_shard_pipeline(m, golden, group, shards, count):
+    """Equal shards on one device: the batch of `count` sets runs as one
+    pipeline of count x shards jobs (several reduction groups, front groups of
+    one job); every folded result equals the single-device context's batch, and
+    set 0 the golden MSM."""
+    n = 1 << 12 if group == 1 else 1 << 10
+    pts = m.fixed_points(group, n)
+    one = m.CHESContext(group, 0, n_exp=10)
+    one.build_table(pts, n)
+    multi = m.CHESContext(group, n_exp=10, devices=[0] * shards)
+    multi.build_table(pts, n)
+    sets = b"".join(bytes(m.gen_scalars(n, 1 if k == 0 else 40 + k)) for k in range(count))
+    got = [m.compress(group, r) for r in multi.mult_batch(sets, count)]
+    want = [m.compress(group, r) for r in one.mult_batch(sets, count)]
+    assert got == want
+    assert got[0].hex() == _golden(golden, group, n)
+    one.close()
+    multi.close()
 
 
 @pytest.mark.parametrize("group,shards", [(1, 3), (2, 2)])

@@ -116,6 +116,7 @@ CASES = {
     "c18": lambda: ches(18),
     "c19": lambda: ches(19),
     "c20": lambda: ches(20),
+    "c20b": lambda: ches(20, 1),
 }
 
 if __name__ == "__main__":
