@@ -868,11 +868,15 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
     host_out_bytes_ = bytes;
   }
   // (group size cap: kFrontGroupDefault, or MSM_FRONT_GROUP=<1..8>; engine.hpp)
+  // (small MSMs on lanes: groups of 2 -- half the front launches, measured
+  // 0.551 -> 0.530 ms per 2^17 MSM and 0.874 -> 0.845 at 2^18; the 2^20 batch
+  // keeps 1, its wider fronts starve the accumulation, r03_front_group_ab.txt)
   static const size_t fg_env = [] {
     const char *e = getenv("MSM_FRONT_GROUP");
-    return (size_t)std::min(kFrontGroup, std::max(1, e ? atoi(e) : kFrontGroupDefault));
+    return e ? (size_t)std::min(kFrontGroup, std::max(1, atoi(e))) : (size_t)0;
   }();
-  const size_t fg_max = packed ? fg_env : 1;
+  const int nl = batch_lanes();
+  const size_t fg_max = !packed ? 1 : fg_env ? fg_env : nl >= 2 ? 2 : (size_t)kFrontGroupDefault;
   // front groups of 1, 1, 2, 4, then fg_max MSMs: the first accumulation
   // starts after one front, and each group's host sets (copied while the earlier
   // groups accumulate: a set copies in ~0.6 ms, an MSM accumulates in ~2.3) are
@@ -885,7 +889,6 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
   // every buffer the loop touches exists before the first launch (an allocation
   // inside the issue loop could synchronise the device)
   const size_t NB = bucket_count(), n = n_;
-  const int nl = batch_lanes();
   for (int b = 0; b < std::max(kBSets, nl); ++b) buckets_[b].ensure(NB * sizeof(Xyzz<typename FieldOf<G>::F>));
   // sized for kGroup whatever this batch's R: a later, larger batch must not
   // reallocate (a hipFree inside the pipelined region would synchronise it)
