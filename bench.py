@@ -845,8 +845,10 @@ def cfg3_multi_context(m, torch, D, one_device, K, W):
         "value": round(N * K / el, 1), "unit": "pairs/s", "ms_per_step": round(el / K * 1e3, 4),
         "sync_ms_per_msm": round(sel * 1e3, 4), "parity_vs_reference": m.compress(1, res[0]).hex() == want,
         "batch_equals_sync": eq, "setup_s": round(setup, 2), "devices": devs,
+        "shards_merged": bool(one_device and D > 1 and os.environ.get("MSM_MULTI_MERGE", "1") != "0"),
         "note": f"configs[3] in ONE process: {D} shards of {n} points (config_file_n_exp_{n_exp}.h) on devices "
-                f"{sorted(set(devs))}, msm_ches_ctx_create_multi, {K} distinct sets from pinned host memory"}}
+                f"{sorted(set(devs))}, msm_ches_ctx_create_multi, {K} distinct sets from pinned host memory; "
+                "shards sharing a device run as one engine over their joint range (csrc/multi.hpp)"}}
 
 
 def _ref_lib(name):

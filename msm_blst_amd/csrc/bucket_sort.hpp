@@ -10,7 +10,7 @@
 //                 (bucket >> fb_bits) -> ghist[bin * ntiles + tile]
 //   (hipcub)      exclusive scan of ghist (bin-major) -> gbase
 //   k_bs_coarse   per tile: LDS rank within (tile, bin) -> coarse-sorted keys/vals
-//   k_bs_fine     one 1024-thread workgroup per coarse bin: LDS histogram over
+//   k_bs_fine     one workgroup (1024 or 256 threads) per coarse bin: LDS histogram over
 //                 its 2^fb_bits buckets, block scan, counts/offsets out, vals
 //                 placed in bucket order in LDS windows and streamed out; also
 //                 the accumulation schedule's class histogram
@@ -153,13 +153,16 @@ static __global__ void __launch_bounds__(256)
   }
 }
 
-// exclusive scan of a[0..n) in LDS by a 1024-thread block (n <= 4096); returns via a
+// exclusive scan of a[0..n) in LDS by a BT-thread block (n <= 4096, so at most
+// 4096 / BT consecutive elements per thread); wsum: BT / 64 words of LDS
+template <int BT>
 __device__ __forceinline__ void block_exclusive_scan_4096(uint32_t *a, int n, uint32_t *wsum) {
+  constexpr int PER = 4096 / BT, NW = BT / 64;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int per = (n + 1023) / 1024;  // <= 4 consecutive elements per thread
-  uint32_t loc[4], s = 0;
+  const int per = (n + BT - 1) / BT;
+  uint32_t loc[PER], s = 0;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < PER; ++k) {
     int i = t * per + k;
     loc[k] = s;
     if (k < per && i < n) s += a[i];
@@ -174,7 +177,7 @@ __device__ __forceinline__ void block_exclusive_scan_4096(uint32_t *a, int n, ui
   __syncthreads();
   if (t == 0) {
     uint32_t run = 0;
-    for (int w = 0; w < 16; ++w) {
+    for (int w = 0; w < NW; ++w) {
       uint32_t x = wsum[w];
       wsum[w] = run;
       run += x;
@@ -183,7 +186,7 @@ __device__ __forceinline__ void block_exclusive_scan_4096(uint32_t *a, int n, ui
   __syncthreads();
   const uint32_t base = wsum[wave] + incl - s;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < PER; ++k) {
     int i = t * per + k;
     if (k < per && i < n) a[i] = base + loc[k];
   }
@@ -207,7 +210,13 @@ constexpr int BS_FINE_CAP = 30 * 1024;                        // staged entries 
 constexpr int BS_FINE_STEP = BS_FINE_CAP - BS_FINE_CAP / 8;   // window stride, leaves slack
 constexpr int BS_FINE_MAXW = 8;
 
-static __global__ void __launch_bounds__(1024)
+//
+// BT = threads per workgroup: 1024 (the default everywhere).  256 (one wave
+// per SIMD, 56 VGPRs) fits beside three k_accumulate waves per SIMD, so a batch
+// front dispatched under an accumulation need not wait for a CU to drain; it
+// measured slower in the batch (Ches::run_jobs, MSM_FINE_BT).
+template <int BT>
+static __global__ void __launch_bounds__(BT)
     k_bs_fine(const uint32_t *__restrict__ okeys, const uint32_t *__restrict__ ovals, int fb_bits, int ncb,
               int ntiles, const uint32_t *__restrict__ gbase, const uint32_t *__restrict__ ghist, uint32_t nb,
               uint32_t *__restrict__ sorted, uint32_t *__restrict__ counts, uint32_t *__restrict__ offsets,
@@ -215,7 +224,7 @@ static __global__ void __launch_bounds__(1024)
   __shared__ uint32_t off[1 << BS_MAX_FB_BITS];
   __shared__ uint8_t win[1 << BS_MAX_FB_BITS];
   __shared__ uint32_t stage[BS_FINE_CAP];
-  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t wsum[BT / 64];
   __shared__ uint32_t wb[BS_FINE_MAXW + 1];
   __shared__ uint32_t cls[256];
   const int FB = 1 << fb_bits;
@@ -231,15 +240,15 @@ static __global__ void __launch_bounds__(1024)
   class_total += (size_t)set * 512;
   const uint32_t nbin = hi - lo;
   for (int f = threadIdx.x; f < FB; f += blockDim.x) off[f] = 0;
-  if (threadIdx.x < 256) cls[threadIdx.x] = 0;
+  for (int c = threadIdx.x; c < 256; c += BT) cls[c] = 0;
   if (threadIdx.x <= BS_FINE_MAXW) wb[threadIdx.x] = nbin;
   __syncthreads();
   constexpr int U = 16, UW = 12;  // loads in flight per thread (histogram / window passes)
-  for (uint32_t e0 = lo; e0 < hi; e0 += U * 1024) {
+  for (uint32_t e0 = lo; e0 < hi; e0 += U * BT) {
     uint32_t kk[U];
 #pragma unroll
     for (int r = 0; r < U; ++r) {
-      uint32_t e = e0 + threadIdx.x + r * 1024;
+      uint32_t e = e0 + threadIdx.x + r * BT;
       kk[r] = e < hi ? okeys[e] : BS_NONE;
     }
 #pragma unroll
@@ -255,8 +264,9 @@ static __global__ void __launch_bounds__(1024)
     }
   }
   __syncthreads();
-  if (threadIdx.x < 256 && cls[threadIdx.x]) atomicAdd(&class_total[threadIdx.x], cls[threadIdx.x]);
-  block_exclusive_scan_4096(off, FB, wsum);
+  for (int c = threadIdx.x; c < 256; c += BT)
+    if (cls[c]) atomicAdd(&class_total[c], cls[c]);
+  block_exclusive_scan_4096<BT>(off, FB, wsum);
   const uint32_t nwin = (nbin + BS_FINE_STEP - 1) / BS_FINE_STEP;
   const bool staged = nwin <= (uint32_t)BS_FINE_MAXW;
   for (int f = threadIdx.x; f < FB; f += blockDim.x) {
@@ -270,11 +280,11 @@ static __global__ void __launch_bounds__(1024)
   }
   __syncthreads();
   if (!staged) {
-    for (uint32_t e0 = lo; e0 < hi; e0 += U * 1024) {
+    for (uint32_t e0 = lo; e0 < hi; e0 += U * BT) {
       uint32_t kk[U], vv[U];
 #pragma unroll
       for (int r = 0; r < U; ++r) {
-        uint32_t e = e0 + threadIdx.x + r * 1024;
+        uint32_t e = e0 + threadIdx.x + r * BT;
         kk[r] = e < hi ? okeys[e] : BS_NONE;
         vv[r] = e < hi ? ovals[e] : 0u;
       }
@@ -293,13 +303,13 @@ static __global__ void __launch_bounds__(1024)
     uint32_t end = nbin;
     for (uint32_t j = k + 1; j < nwin; ++j)
       if (wb[j] < end) end = wb[j];
-    for (uint32_t e0 = lo; e0 < hi; e0 += UW * 1024) {
+    for (uint32_t e0 = lo; e0 < hi; e0 += UW * BT) {
       // keys and vals in one round trip (a dependent vals load per key would
       // double the latency-bound passes); vals of other windows are re-read
       uint32_t kk[UW], vv[UW];
 #pragma unroll
       for (int r = 0; r < UW; ++r) {
-        uint32_t e = e0 + threadIdx.x + r * 1024;
+        uint32_t e = e0 + threadIdx.x + r * BT;
         kk[r] = e < hi ? okeys[e] : BS_NONE;
         vv[r] = e < hi ? ovals[e] : 0u;
       }
@@ -315,7 +325,7 @@ static __global__ void __launch_bounds__(1024)
     }
     __syncthreads();
     const uint32_t nst = min(end - base, (uint32_t)BS_FINE_CAP);
-    for (uint32_t i = threadIdx.x; i < nst; i += 1024) sorted[lo + base + i] = stage[i];
+    for (uint32_t i = threadIdx.x; i < nst; i += BT) sorted[lo + base + i] = stage[i];
     __syncthreads();
   }
 }
@@ -332,7 +342,7 @@ static __global__ void __launch_bounds__(1024)
 // The bucket's count and payload offset are written beside its id in schedule
 // order (scnt / soff), so the accumulation reads them coalesced by lane instead
 // of two random 4-B loads (two 64-B lines) per bucket.
-static __global__ void __launch_bounds__(256)
+static __global__ void __launch_bounds__(256, 6)  // <= 80 VGPRs: fits beside three k_accumulate waves per SIMD
     k_sched_scatter(const uint32_t *__restrict__ counts, const uint32_t *__restrict__ offsets, uint32_t nb,
                     uint32_t *__restrict__ class_total, uint32_t *__restrict__ order, uint32_t *__restrict__ scnt,
                     uint32_t *__restrict__ soff) {
@@ -359,13 +369,12 @@ static __global__ void __launch_bounds__(256)
   __syncthreads();
   uint32_t cbase = incl - v;
   for (uint32_t w = 0; w < wave; ++w) cbase += wsum[w];
-  uint32_t cls[SCHED_PER_THREAD], rank[SCHED_PER_THREAD], cnt[SCHED_PER_THREAD];
+  uint32_t rank[SCHED_PER_THREAD], cnt[SCHED_PER_THREAD];  // (the class is recomputed from the count)
 #pragma unroll
   for (int r = 0; r < SCHED_PER_THREAD; ++r) {
     const uint32_t b = b0 + r * 256 + t;
     cnt[r] = b < nb ? counts[b] : 0u;
-    cls[r] = sched_class(cnt[r]);
-    rank[r] = b < nb ? atomicAdd(&h[cls[r]], 1u) : 0u;
+    rank[r] = b < nb ? atomicAdd(&h[sched_class(cnt[r])], 1u) : 0u;
   }
   __syncthreads();
   if (h[t]) base[t] = cbase + atomicAdd(&class_total[256 + t], h[t]);
@@ -374,7 +383,7 @@ static __global__ void __launch_bounds__(256)
   for (int r = 0; r < SCHED_PER_THREAD; ++r) {
     const uint32_t b = b0 + r * 256 + t;
     if (b < nb) {
-      const uint32_t pos = base[cls[r]] + rank[r];
+      const uint32_t pos = base[sched_class(cnt[r])] + rank[r];
       order[pos] = b;
       scnt[pos] = cnt[r];
       soff[pos] = offsets[b];

@@ -591,7 +591,8 @@ void Ches<G>::plan_buckets(size_t n) {
 
 // Accumulation lanes of a batch (run_batch): 2 when one accumulation's lanes
 // (one per bucket for G1, two for G2) fill fewer than ~3 rounds of the chip's
-// wave slots (1024 SIMDs x 3 waves x 64 lanes), else 1.  MSM_BATCH_LANES=1|2|3
+// wave slots (1024 SIMDs x the kernel's waves per SIMD x 64 lanes: 3 for
+// k_accumulate<1>, 2 for k_accumulate2p), else 1.  MSM_BATCH_LANES=1|2|3
 // overrides.
 template <int G>
 int Ches<G>::batch_lanes() const {
@@ -601,7 +602,7 @@ int Ches<G>::batch_lanes() const {
   }();
   if (env) return env;
   const size_t lanes = bucket_count() * (G == 2 ? 2 : 1);
-  return lanes < (size_t)3 * 3 * 1024 * 64 ? 2 : 1;
+  return lanes < (size_t)3 * (G == 2 ? 2 : 3) * 1024 * 64 ? 2 : 1;
 }
 
 template <int G>
@@ -699,9 +700,10 @@ void Ches<G>::get_table(void *out, size_t first, size_t count, hipStream_t s) {
 
 template <int G>
 void Ches<G>::digits_sort(hipStream_t s, const uint8_t *d_scalars, size_t stride, size_t set_stride, int nsets,
-                          int set) {
+                          int set, int fine_bt) {
   const size_t n = n_, h = (size_t)p_.h, ne = n * h, NB = bucket_count();
   ChesFrontSet &f = fs_[set];
+  f.sort.fine_bt = fine_bt;
   f.sorted.ensure(ne * nsets * 4 + 64);  // + the accumulation's 16-B payload window past a run's end
   f.counts.ensure(NB * nsets * 4);
   f.offsets.ensure(NB * nsets * 4);
@@ -876,6 +878,14 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
     return e ? (size_t)std::min(kFrontGroup, std::max(1, atoi(e))) : (size_t)0;
   }();
   const int nl = batch_lanes();
+  // the batch fronts' fine-pass workgroup (bucket_sort.hpp k_bs_fine): 1024
+  // threads; MSM_FINE_BT=256 selects the variant that fits beside three
+  // accumulation waves per SIMD -- measured slower (H2D 408-411 vs 415-420 M,
+  // resident 423-429 vs 434-440 M pairs/s, profiles/r04_fine_bt_ab.txt)
+  static const int fine_bt = [] {
+    const char *e = getenv("MSM_FINE_BT");
+    return e && atoi(e) == 256 ? 256 : 1024;
+  }();
   const size_t fg_max = !packed ? 1 : fg_env ? fg_env : nl >= 2 ? 2 : (size_t)kFrontGroupDefault;
   // front groups of 1, 1, 2, 4, then fg_max MSMs: the first accumulation
   // starts after one front, and each group's host sets (copied while the earlier
@@ -1008,7 +1018,8 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
         MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, eva[last - d], 0));
     }
     const uint8_t *src = copied ? slots(g) : job_scalars(fgb[g]);
-    digits_sort(fstream_, src, stride, copied ? sslot : jstride, (int)(fgb[g + 1] - fgb[g]), (int)(g % nfr));
+    digits_sort(fstream_, src, stride, copied ? sslot : jstride, (int)(fgb[g + 1] - fgb[g]), (int)(g % nfr),
+                fine_bt);
     MSM_HIP_CHECK(hipEventRecord(evf[g], fstream_));
   };
   for (size_t g = 0; g < nsg; ++g) copy_group(g);

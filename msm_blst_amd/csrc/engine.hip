@@ -74,9 +74,14 @@ void BucketSort::finish(hipStream_t s, const Geom &g, size_t ne, uint32_t nb, ui
   (void)ne;
   const int fb_bits = g.fb_bits, ncb = g.ncb, ntiles = g.ntiles;
   const size_t nw = groups(nb);
-  hipLaunchKernelGGL(k_bs_fine, dim3(ncb, nsets), dim3(1024), 0, s, okeys.as<uint32_t>(), ovals.as<uint32_t>(),
-                     fb_bits, ncb, ntiles, gbase.as<uint32_t>(), ghist.as<uint32_t>(), nb, sorted, counts, offsets,
-                     classes.as<uint32_t>(), nsets);
+  if (fine_bt == 256)
+    hipLaunchKernelGGL(k_bs_fine<256>, dim3(ncb, nsets), dim3(256), 0, s, okeys.as<uint32_t>(),
+                       ovals.as<uint32_t>(), fb_bits, ncb, ntiles, gbase.as<uint32_t>(), ghist.as<uint32_t>(), nb,
+                       sorted, counts, offsets, classes.as<uint32_t>(), nsets);
+  else
+    hipLaunchKernelGGL(k_bs_fine<1024>, dim3(ncb, nsets), dim3(1024), 0, s, okeys.as<uint32_t>(),
+                       ovals.as<uint32_t>(), fb_bits, ncb, ntiles, gbase.as<uint32_t>(), ghist.as<uint32_t>(), nb,
+                       sorted, counts, offsets, classes.as<uint32_t>(), nsets);
   MSM_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(k_sched_scatter, dim3(nblk(nb, SCHED_PER_BLOCK), nsets), dim3(256), 0, s, counts, offsets, nb,
                      classes.as<uint32_t>(), order, scnt.as<uint32_t>(), soff.as<uint32_t>());

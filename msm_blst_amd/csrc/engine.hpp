@@ -77,6 +77,7 @@ struct BucketSort {
   // and the interleaved payload
   DevBuf scnt, soff, wbase, ipay;
   size_t ipay_stride = 0;  // interleaved entries per set (ne + BS_IPAY_SLACK)
+  int fine_bt = 1024;      // k_bs_fine workgroup size: 1024 alone, 256 under a batch's accumulations
   static size_t groups(size_t nb) { return (nb + 63) / 64; }
   // set `set` of the last run (nb buckets per set); order/sorted as passed to run
   AccSched sched(const uint32_t *order, const uint32_t *sorted, size_t set, size_t nb) const {
@@ -418,7 +419,10 @@ class Ches {
   std::vector<hipEvent_t> bev_;     // batch dependency events, one per (MSM, stage)
   std::vector<hipEvent_t> acc_ev_;  // batch profiling: events around each accumulation
   // digits + sort of nsets scalar sets (set_stride bytes apart) into front set `set`
-  void digits_sort(hipStream_t s, const uint8_t *d_scalars, size_t stride, size_t set_stride, int nsets, int set);
+  // fine_bt: k_bs_fine workgroup size (1024 alone; 256 for a batch front that
+  // runs under accumulations, bucket_sort.hpp)
+  void digits_sort(hipStream_t s, const uint8_t *d_scalars, size_t stride, size_t set_stride, int nsets, int set,
+                   int fine_bt = 1024);
   // accumulation of scalar set r of front set `set` into bucket set bset
   // (table: the table_ of this engine, or of a segment's engine in run_jobs)
   void accumulate(hipStream_t s, int set, int r, int bset, const void *table = nullptr);

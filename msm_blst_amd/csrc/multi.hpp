@@ -20,8 +20,16 @@
 // binding splits points x windows over threads (bindings/go/blst.go:2064-2197),
 // which would replicate points and tables on every GPU, so points are sharded.
 //
-// Shards may share a device (devices = {0, 0, ...}): each engine keeps its own
-// buffers and streams, which is how the 1-GPU tests exercise the 8-shard fold.
+// Shards may share a device (devices = {0, 0, ...}).  Consecutive shards on one
+// device are merged into ONE engine over their joint point range (the table
+// layout is point-major, so their rows are one contiguous range, and the sum
+// of their partials is the MSM of that range): a device then runs one MSM per
+// scalar set -- one front, accumulation, level 0 and reduction tail -- instead
+// of one per shard (configs[3]'s 8 x 2^18 shards on one device: 8 latency-bound
+// 2^18 pipelines became one 2^21 MSM).  MSM_MULTI_MERGE=0 (read when a context
+// is created) keeps one engine per shard -- how the 1-GPU tests exercise the
+// shard fold -- and MSM_MULTI_PIPELINE=0 additionally runs those engines
+// concurrently instead of as one pipeline over (set, shard) jobs.
 #pragma once
 #include <condition_variable>
 #include <cstring>
@@ -43,6 +51,7 @@ class ChesMulti {
   typedef typename HostField<G>::F HF;
   struct Shard {
     int device = 0;
+    int nlog = 1;             // caller's shards merged into this one (consecutive, same device)
     size_t start = 0, n = 0;  // global point range [start, start + n)
     std::unique_ptr<Ches<G>> eng;
     DevBuf scal;               // host scalars of this shard, per call
@@ -60,21 +69,29 @@ class ChesMulti {
     std::exception_ptr err;
   };
 
-  ChesMulti(const std::vector<int> &devices, const ChesParams &p) : p_(p) {
+  ChesMulti(const std::vector<int> &devices, const ChesParams &p) : p_(p), nlogical_(devices.size()) {
     if (devices.empty()) throw std::runtime_error("ChesMulti: no devices");
-    shards_ = std::vector<Shard>(devices.size());
+    const char *me = getenv("MSM_MULTI_MERGE"), *pe = getenv("MSM_MULTI_PIPELINE");
+    const bool merge = !me || atoi(me) != 0;
+    pipeline_ = !pe || atoi(pe) != 0;
+    std::vector<std::pair<int, int>> groups;  // (device, caller shards)
+    for (int d : devices)
+      if (merge && !groups.empty() && groups.back().first == d) ++groups.back().second;
+      else groups.push_back({d, 1});
+    shards_ = std::vector<Shard>(groups.size());
     try {
-      for (size_t g = 0; g < devices.size(); ++g) {
+      for (size_t g = 0; g < groups.size(); ++g) {
         Shard &s = shards_[g];
-        s.device = devices[g];
+        s.device = groups[g].first;
+        s.nlog = groups[g].second;
         s.eng = std::make_unique<Ches<G>>(s.device, p);
-        if (devices.size() > 1) {
+        if (groups.size() > 1) {
           DeviceGuard dg(s.device);
           MSM_HIP_CHECK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
         }
       }
-      if (devices.size() > 1) {
-        workers_ = std::vector<Worker>(devices.size());
+      if (groups.size() > 1) {
+        workers_ = std::vector<Worker>(groups.size());
         for (Worker &w : workers_) w.th = std::thread([&w] { work(w); });
       }
     } catch (...) {
@@ -85,8 +102,8 @@ class ChesMulti {
   ~ChesMulti() { release(); }
   ChesMulti(const ChesMulti &) = delete;
   ChesMulti &operator=(const ChesMulti &) = delete;
-  size_t nshards() const { return shards_.size(); }
-  const Shard &shard(size_t k) const { return shards_[k]; }
+  size_t nshards() const { return nlogical_; }  // the caller's shards (merged ones included)
+  size_t engines() const { return shards_.size(); }
   Ches<G> &front() { return *shards_[0].eng; }
   const Ches<G> &front() const { return *shards_[0].eng; }
   const ChesParams &params() const { return p_; }
@@ -208,28 +225,29 @@ class ChesMulti {
 
  private:
   ChesParams p_;
+  size_t nlogical_ = 1;
+  bool pipeline_ = true;
   std::vector<Shard> shards_;
   size_t n_ = 0;
 
   // all shards on one device with equal point counts (MSM_MULTI_PIPELINE=0: one
   // engine per shard, concurrently, as on separate devices)
   bool one_device_pipeline() const {
-    static const bool env = [] {
-      const char *e = getenv("MSM_MULTI_PIPELINE");
-      return !e || atoi(e) != 0;
-    }();
-    if (!env || shards_.size() < 2 || shards_[0].n == 0) return false;
+    if (!pipeline_ || shards_.size() < 2 || shards_[0].n == 0) return false;
     for (const Shard &sh : shards_)
       if (sh.device != shards_[0].device || sh.n != shards_[0].n) return false;
     return true;
   }
+  // balanced contiguous ranges over the caller's shards; a merged shard owns the
+  // union of its members' ranges
   void split(size_t n) {
-    const size_t S = shards_.size(), base = n / S, rem = n % S;
-    size_t at = 0;
-    for (size_t g = 0; g < S; ++g) {
-      shards_[g].start = at;
-      shards_[g].n = base + (g < rem ? 1 : 0);
-      at += shards_[g].n;
+    const size_t L = nlogical_, base = n / L, rem = n % L;
+    size_t at = 0, l = 0;
+    for (Shard &sh : shards_) {
+      sh.start = at;
+      sh.n = 0;
+      for (int k = 0; k < sh.nlog; ++k, ++l) sh.n += base + (l < rem ? 1 : 0);
+      at += sh.n;
     }
     n_ = n;
   }

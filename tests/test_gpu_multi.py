@@ -1,9 +1,23 @@
 """The C/C++ multi-device CHES path (msm_ches_ctx_create_multi, csrc/multi.hpp):
 points sharded contiguously over several devices of ONE process, per-shard
 tables, concurrent per-shard MSMs and the exact host fold of the partials
-(SURVEY 8e).  On the 1-GPU box the shards share device 0 (devices = [0]*k),
-which exercises the same split / route / fold code the 8-GPU node runs."""
+(SURVEY 8e).  On the 1-GPU box the shards share device 0 (devices = [0]*k).
+Shards sharing a device are merged into one engine by default (multi.hpp);
+`shard_mode` also runs the unmerged paths the 8-GPU node takes -- one engine
+per shard as one pipeline over (set, shard) jobs ("pipeline") or concurrently
+("engines") -- so the split / route / fold code is exercised on one GPU."""
 import pytest
+
+MODES = {"merged": {}, "pipeline": {"MSM_MULTI_MERGE": "0"},
+         "engines": {"MSM_MULTI_MERGE": "0", "MSM_MULTI_PIPELINE": "0"}}
+
+
+def _mode(monkeypatch, mode):
+    """set the shard mode for contexts created after this call (read at creation)"""
+    for k in ("MSM_MULTI_MERGE", "MSM_MULTI_PIPELINE"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in MODES[mode].items():
+        monkeypatch.setenv(k, v)
 
 pytestmark = pytest.mark.gpu
 
@@ -21,17 +35,20 @@ def _golden(golden, group, n, seed=1):
             if c["n"] == n and c["seed"] == seed and c["case"] == "rand" and c["nbits"] == 255][0]["compressed"]
 
 
-def test_configs3_2e21_over_8_shards(m, golden):
+@pytest.mark.parametrize("mode", ["merged", "pipeline"])
+def test_configs3_2e21_over_8_shards(m, golden, monkeypatch, mode):
     """BASELINE configs[3]: n = 2^21 over 8 shards, config_file_n_exp_18 per shard,
     against the reference's golden MSM of 2^21 points."""
+    _mode(monkeypatch, mode)
     n = 1 << 21
     ctx = m.CHESContext(1, n_exp=18, devices=[0] * 8)
     assert ctx.shards() == 8
     ctx.build_table(m.fixed_points(1, n), n)
     sc = m.gen_scalars(n, 1)
     assert m.compress(1, ctx.mult(sc)).hex() == _golden(golden, 1, n)
-    # the batch: all 8 shards share device 0, so it runs as ONE pipeline over
-    # (set, shard) jobs (Ches::run_jobs), each job reading its shard's table
+    # the batch: all 8 shards share device 0, so it runs as one 2^21 MSM per set
+    # (merged) or as ONE pipeline over (set, shard) jobs (Ches::run_jobs), each
+    # job reading its shard's table
     sets = bytes(sc) + bytes(m.gen_scalars(n, 7))
     got = ctx.mult_batch(sets, 2)
     assert m.compress(1, got[0]).hex() == _golden(golden, 1, n)
@@ -39,12 +56,14 @@ def test_configs3_2e21_over_8_shards(m, golden):
     ctx.close()
 
 
+@pytest.mark.parametrize("mode", ["merged", "pipeline", "engines"])
 @pytest.mark.parametrize("group,shards,count", [(1, 4, 6), (2, 2, 3)])
-def test_one_device_shard_pipeline(m, golden, group, shards, count):
+def test_one_device_shard_pipeline(m, golden, monkeypatch, group, shards, count, mode):
     """Equal shards on one device: the batch of `count` sets runs as one
     pipeline of count x shards jobs (several reduction groups, front groups of
     one job); every folded result equals the single-device context's batch, and
     set 0 the golden MSM."""
+    _mode(monkeypatch, mode)
     n = 1 << 12 if group == 1 else 1 << 10
     pts = m.fixed_points(group, n)
     one = m.CHESContext(group, 0, n_exp=10)
@@ -60,11 +79,13 @@ def test_one_device_shard_pipeline(m, golden, group, shards, count):
     multi.close()
 
 
+@pytest.mark.parametrize("mode", ["merged", "engines"])
 @pytest.mark.parametrize("group,shards", [(1, 3), (2, 2)])
-def test_uneven_shards_table_layout_and_batch(m, golden, group, shards):
+def test_uneven_shards_table_layout_and_batch(m, golden, monkeypatch, group, shards, mode):
     """n = 2^10 over an uneven split (341/341/342): the sharded table reads back
     byte-identical to the single-device table in the reference layout; mult and
     a 4-set batch equal the golden / single-device results."""
+    _mode(monkeypatch, mode)
     n = 1 << 10
     pts = m.fixed_points(group, n)
     one = m.CHESContext(group, 0, n_exp=10)
@@ -84,9 +105,11 @@ def test_uneven_shards_table_layout_and_batch(m, golden, group, shards):
     multi.close()
 
 
-def test_sharded_table_file_roundtrip(m, golden, tmp_path):
+@pytest.mark.parametrize("mode", ["merged", "engines"])
+def test_sharded_table_file_roundtrip(m, golden, tmp_path, monkeypatch, mode):
     """save_table / load_table on a sharded context keep the reference layout:
     a file written by a 2-shard context loads into a single-device one."""
+    _mode(monkeypatch, mode)
     n = 1 << 10
     multi = m.CHESContext(1, n_exp=10, devices=[0, 0])
     multi.build_table(m.fixed_points(1, n), n)
