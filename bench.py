@@ -58,19 +58,22 @@ CPU_THREADS = 16               # the GPU box's CPU share per GPU (16 threads)
 DEFAULT_BETA = {}              # log_n -> ches_config_files variant used by default; _beta at 2^20 measured slower
 
 
-def isa_mads_per_madd(path=os.path.join(REPO, "profiles", "r04_isa_counts.txt")):
-    """v_mad_u64_u32 per G1 xyzz madd on its main path, from the gfx950 ISA of
-    the shipped field code (tools/isa_report.sh): the madd is 6 products
-    (U2, S2, PPP, Q, ZZ3, ZZZ3), 2 squares (PP, R^2) and one fused two-product
-    sum (Y3 = R (Q - X3) - S1 PPP), ec.hpp xyzz_madd."""
+def isa_mads_per_madd(G=1, path=os.path.join(REPO, "profiles", "r04_isa_counts.txt")):
+    """v_mad_u64_u32 per xyzz madd on its main path, from the gfx950 ISA of the
+    shipped field code (tools/isa_report.sh): the madd is 6 products (U2, S2,
+    PPP, Q, ZZ3, ZZZ3), 2 squares (PP, R^2) and one fused two-product sum
+    (Y3 = R (Q - X3) - S1 PPP), ec.hpp xyzz_madd.  G1: Fp ops on one lane; G2:
+    the lane-pair Fp2 ops (fp2l.hpp), counted per lane, times the two lanes."""
     import re
+    keys = (("k_op_fp_mulP", "k_op_fp_sqr", "k_op_fp_mul2") if G == 1 else
+            ("k_op_g2l_mul_bs", "k_op_g2l_sqr", "k_op_g2l_mul_sub"))
     try:
         txt = open(path).read()
-        cnt = {k: int(re.search(k + r"\w*\n\s+vgpr \d+ scratch \d+ total \d+ v_mad_u64_u32 (\d+)", txt).group(1))
-               for k in ("k_op_fp_mulP", "k_op_fp_sqr", "k_op_fp_mul2")}
-        return 6 * cnt["k_op_fp_mulP"] + 2 * cnt["k_op_fp_sqr"] + cnt["k_op_fp_mul2"], os.path.basename(path)
+        cnt = [int(re.search(k + r"\w*\n\s+vgpr \d+ scratch \d+ total \d+ v_mad_u64_u32 (\d+)", txt).group(1))
+               for k in keys]
+        return (6 * cnt[0] + 2 * cnt[1] + cnt[2]) * (1 if G == 1 else 2), os.path.basename(path)
     except Exception:
-        return 3567, "profiles/r03_isa_counts.txt (constant)"
+        return (3567, "profiles/r03_isa_counts.txt (constant)") if G == 1 else (None, "no lane-pair counts")
 
 
 def log(*a):
@@ -405,7 +408,7 @@ def main():
             traffic = None
     fpm_per_madd = FPMUL_PER_MADD if G == 1 else 28   # Fp2: 8M + 2S = 8*3 + 2*2 Fp-mul
     fpmul_rate = madds * fpm_per_madd / acc_s
-    mads, mads_src = isa_mads_per_madd()
+    mads, mads_src = isa_mads_per_madd(G)
 
     parity = golden_ok if golden_ok is not None else cross
     if batch_eq_sync is False:
@@ -444,11 +447,12 @@ def main():
                           "alone_basis": "the same kernel in one synchronous MSM (phases_ms.accumulate): no front or "
                                          "reduction of a neighbouring MSM shares its SIMDs",
                           # hardware-anchored: v_mad_u64_u32 issued per launch vs the measured chip mad rate
-                          "mad_frac": round(madds * mads / acc_s / MAD_RATE, 4) if G == 1 else None,
+                          "mad_frac": round(madds * mads / acc_s / MAD_RATE, 4) if mads else None,
                           "mad_frac_alone": (round(madds * mads / (phases["accumulate"] / 1e3) / MAD_RATE, 4)
-                                             if G == 1 and phases.get("accumulate") else None),
-                          "mads_per_madd": mads if G == 1 else None, "mad_rate_peak": MAD_RATE,
-                          "mad_basis": (f"{madds} madds x {mads} v_mad_u64_u32 (6 mul + 2 sqr + 1 two-product sum, "
+                                             if mads and phases.get("accumulate") else None),
+                          "mads_per_madd": mads, "mad_rate_peak": MAD_RATE,
+                          "mad_basis": (f"{madds} madds x {mads} v_mad_u64_u32 (6 mul + 2 sqr + 1 two-product sum"
+                                        f"{'' if G == 1 else ' of Fp2 on a lane pair, both lanes'}, "
                                         f"gfx950 ISA counts {mads_src}) / kernel time / {MAD_RATE / 1e12:.2f} T "
                                         f"mad/s (profiles/r02_instr_rate.txt)")},
         "phases_ms": {k: round(v, 4) for k, v in phases.items()},

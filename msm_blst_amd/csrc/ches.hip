@@ -844,8 +844,12 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
     int least = 0, greatest = 0;
     MSM_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
     MSM_HIP_CHECK(hipStreamCreateWithPriority(&fstream_, hipStreamNonBlocking, greatest));
+    static const bool tail_hi = [] {  // A/B knob: reduction streams at the front's (greatest) priority
+      const char *e = getenv("MSM_TAIL_PRIO");
+      return e && atoi(e) != 0;
+    }();
     for (int t = 0; t < kBSets; ++t) {
-      MSM_HIP_CHECK(hipStreamCreateWithPriority(&tails_[t], hipStreamNonBlocking, 0));
+      MSM_HIP_CHECK(hipStreamCreateWithPriority(&tails_[t], hipStreamNonBlocking, tail_hi ? greatest : 0));
       MSM_HIP_CHECK(hipEventCreateWithFlags(&ev_tail_[t], hipEventDisableTiming));
     }
     MSM_HIP_CHECK(hipStreamCreateWithFlags(&cstream_, hipStreamNonBlocking));

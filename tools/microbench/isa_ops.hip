@@ -24,6 +24,25 @@ __global__ void k_op_fp_mul2(const Fp *a, const Fp *b, Fp *r) {
   fp_mul2(z, x, y, u, v);
   r[t] = z;
 }
+// G2 on lane pairs (fp2l.hpp): the three products of the lane-pair madd, per lane
+__global__ void k_op_g2l_mul_bs(const Fp2L *a, const Fp2L *b, Fp2L *r) {
+  const int t = threadIdx.x;
+  Fp2L x = a[t], y = b[t], z;
+  f_mul_bs(z, x, y);
+  r[t] = z;
+}
+__global__ void k_op_g2l_sqr(const Fp2L *a, Fp2L *r) {
+  const int t = threadIdx.x;
+  Fp2L x = a[t], z;
+  f_sqr(z, x);
+  r[t] = z;
+}
+__global__ void k_op_g2l_mul_sub(const Fp2L *a, const Fp2L *b, Fp2L *r) {
+  const int t = threadIdx.x;
+  Fp2L x = a[t], y = b[t], u = a[t + 64], v = b[t + 64], z;
+  f_mul_sub(z, x, y, u, v);
+  r[t] = z;
+}
 __global__ void __launch_bounds__(256, 3) k_op_g1_madd(const Xyzz<Fp> *acc, const Aff<Fp> *p, Xyzz<Fp> *r) {
   const int t = threadIdx.x;
   Xyzz<Fp> q = acc[t];
