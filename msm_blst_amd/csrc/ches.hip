@@ -432,13 +432,21 @@ void WeightedReducer<G>::ensure_group(int set, int nmsm) {
 }
 
 template <int G>
-void WeightedReducer<G>::launch_head_slot(hipStream_t s, const void *Sbuf, int set, int slot) {
+typename WeightedReducer<G>::HeadArgs WeightedReducer<G>::head_args(int set, int slot) {
   typedef typename FieldOf<G>::F F;
   const bool only = nout_.size() == 1;  // level 0 is also the last level
   Xyzz<F> *dst = only ? dense_buf_[set].as<Xyzz<F>>() + (size_t)slot * dense_slots()
                       : part_[set][0].as<Xyzz<F>>() + (size_t)slot * maxp_;
   const uint32_t *ix = only ? idx_.as<uint32_t>() + final_perm_off_ : idx_.as<uint32_t>();
-  launch_segsum<G>(s, reinterpret_cast<const Xyzz<F> *>(Sbuf), ix, starts_[0].as<uint32_t>(), dst, nout_[0]);
+  return HeadArgs{ix, starts_[0].as<uint32_t>(), dst, nout_[0]};
+}
+
+template <int G>
+void WeightedReducer<G>::launch_head_slot(hipStream_t s, const void *Sbuf, int set, int slot) {
+  typedef typename FieldOf<G>::F F;
+  const HeadArgs a = head_args(set, slot);
+  launch_segsum<G>(s, reinterpret_cast<const Xyzz<F> *>(Sbuf), a.idx, a.starts, static_cast<Xyzz<F> *>(a.dst),
+                   a.nout);
   MSM_HIP_CHECK(hipGetLastError());
 }
 
@@ -782,6 +790,25 @@ void Ches<G>::accumulate(hipStream_t s, int set, int r, int bset, const void *ta
 }
 
 template <int G>
+void Ches<G>::accumulate_l0(hipStream_t s, int set, int r, int bset, const void *table, int l0_bset, int gset,
+                            int slot, int l0_last) {
+  if constexpr (G != 1) {
+    throw std::runtime_error("accumulate_l0: G1 only");
+  } else {
+    const size_t NB = bucket_count();
+    ChesFrontSet &f = fs_[set];
+    const typename WeightedReducer<G>::HeadArgs a = red_.head_args(gset, slot);
+    const unsigned l0b = (unsigned)((a.nout + 255) / 256), accb = (unsigned)((NB + 255) / 256);
+    hipLaunchKernelGGL((k_accumulate_l0<AffP<Fp>>), dim3(accb + l0b), dim3(256), 0, s,
+                       f.sort.sched(f.order.as<uint32_t>(), f.sorted.as<uint32_t>(), r, NB),
+                       table ? static_cast<const AffP<Fp> *>(table) : table_.as<AffP<Fp>>(), buckets_[bset].as<Xyzz<Fp>>(),
+                       NB, buckets_[l0_bset].as<Xyzz<Fp>>(), a.idx, a.starts, static_cast<Xyzz<Fp> *>(a.dst), a.nout,
+                       l0b, l0_last);
+    MSM_HIP_CHECK(hipGetLastError());
+  }
+}
+
+template <int G>
 void Ches<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, hfp::Jac<HF> *out) {
   DeviceGuard g(dev_);
   if (stride < 32) throw std::runtime_error("CHES scalars must be 32-byte strings");
@@ -1082,7 +1109,58 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
       }
     }
   }
-  for (size_t g = 0; g < (nl >= 2 ? 0 : nfg); ++g) {
+  // Level 0 inside the next accumulation's grid (G1, MSM_L0_FUSE=1: its
+  // workgroups first, =2: last; k_accumulate_l0): MSM k's launch also runs
+  // level 0 of MSM k - 1 on the caller's stream, the last MSM's level 0 runs
+  // alone after the loop, and reducer set q % 2 is reused by group q + 2 only
+  // after tail q (event evt[q]: level 0 no longer runs on the tail's stream).
+  static const int fuse_env = [] {
+    const char *e = getenv("MSM_L0_FUSE");
+    return e ? std::max(0, std::min(2, atoi(e))) : 0;
+  }();
+  const int fuse = G == 1 && nl < 2 ? fuse_env : 0;
+  auto l0_group_tail = [&](size_t p) {  // after level 0 of MSM p (recorded as evh[p] on s)
+    const size_t pq = p / R, pslot = p % R;
+    if (pslot + 1 != R && p + 1 != count) return;
+    hipStream_t ts = tails_[pq % 2];
+    MSM_HIP_CHECK(hipStreamWaitEvent(ts, evh[p], 0));
+    red_.launch_tail_group(ts, (int)(pq % 2), (int)pslot + 1);
+    red_.copy_out_group(ts, (int)(pq % 2), (int)pslot + 1, (uint8_t *)host_out_ + (p - pslot) * ob);
+    MSM_HIP_CHECK(hipEventRecord(evt[pq], ts));
+  };
+  auto l0_set_free = [&](size_t p) {  // level 0 of MSM p may write its reducer set
+    const size_t pq = p / R;
+    if (p % R == 0 && pq >= 2) MSM_HIP_CHECK(hipStreamWaitEvent(s, evt[pq - 2], 0));
+  };
+  for (size_t g = 0; g < (nl >= 2 || !fuse ? 0 : nfg); ++g) {
+    copy_group(g + nsg);
+    front_group(g + nfr - 1);
+    MSM_HIP_CHECK(hipStreamWaitEvent(s, evf[g], 0));
+    for (size_t k = fgb[g]; k < fgb[g + 1]; ++k) {
+      const int bset = (int)(k % kBSets);
+      if (k >= 1) l0_set_free(k - 1);
+      if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k], s));
+      if (k >= 1)
+        accumulate_l0(s, (int)(g % nfr), (int)(k - fgb[g]), bset, job_table(k), (int)((k - 1) % kBSets),
+                      (int)(((k - 1) / R) % 2), (int)((k - 1) % R), fuse == 2);
+      else
+        accumulate(s, (int)(g % nfr), (int)(k - fgb[g]), bset, job_table(k));
+      if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k + 1], s));
+      MSM_HIP_CHECK(hipEventRecord(eva[k], s));
+      if (k >= 1) {
+        MSM_HIP_CHECK(hipEventRecord(evh[k - 1], s));
+        l0_group_tail(k - 1);
+      }
+    }
+  }
+  if (fuse && nl < 2) {  // level 0 of the last MSM, alone
+    const size_t p = count - 1;
+    l0_set_free(p);
+    red_.launch_head_slot(s, buckets_[p % kBSets].p, (int)((p / R) % 2), (int)(p % R));
+    MSM_HIP_CHECK(hipEventRecord(evh[p], s));
+    l0_group_tail(p);
+  }
+  for (size_t g = 0; g < (nl >= 2 || fuse ? 0 : nfg); ++g) {
     copy_group(g + nsg);
     front_group(g + nfr - 1);  // may start as soon as group g - 1's accumulations release its front set
     MSM_HIP_CHECK(hipStreamWaitEvent(s, evf[g], 0));

@@ -529,15 +529,10 @@ static __global__ void __launch_bounds__(256)
 // for each of gridDim.y MSMs of a batch group: MSM blockIdx.y reads src +
 // y src_stride and writes dst + y dst_stride (the same plan for every MSM)
 template <int G>
-static __global__ void __launch_bounds__(256)
-    k_segsum(const Xyzz<typename FieldOf<G>::F> *__restrict__ src, const uint32_t *__restrict__ idx,
-             const uint32_t *__restrict__ starts, Xyzz<typename FieldOf<G>::F> *__restrict__ dst, size_t nout,
-             size_t src_stride, size_t dst_stride) {
+__device__ __forceinline__ void segsum_one(const Xyzz<typename FieldOf<G>::F> *__restrict__ src,
+                                           const uint32_t *__restrict__ idx, const uint32_t *__restrict__ starts,
+                                           Xyzz<typename FieldOf<G>::F> *__restrict__ dst, size_t t) {
   typedef typename FieldOf<G>::F F;
-  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nout) return;
-  src += blockIdx.y * src_stride;
-  dst += blockIdx.y * dst_stride;
   uint32_t lo = starts[t], hi = starts[t + 1];
   Xyzz<F> acc;
   if (lo == hi) {
@@ -562,6 +557,42 @@ static __global__ void __launch_bounds__(256)
 #endif
   }
   st16(&dst[t], acc);
+}
+template <int G>
+static __global__ void __launch_bounds__(256)
+    k_segsum(const Xyzz<typename FieldOf<G>::F> *__restrict__ src, const uint32_t *__restrict__ idx,
+             const uint32_t *__restrict__ starts, Xyzz<typename FieldOf<G>::F> *__restrict__ dst, size_t nout,
+             size_t src_stride, size_t dst_stride) {
+  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nout) return;
+  segsum_one<G>(src + blockIdx.y * src_stride, idx, starts, dst + blockIdx.y * dst_stride, t);
+}
+
+// Accumulation of MSM k and level 0 of MSM k - 1 in ONE grid (the G1 batch,
+// Ches::run_jobs): the first l0_blocks workgroups are level-0 segment sums of
+// the previous MSM's buckets (k_segsum), the rest the accumulation of this
+// one (k_accumulate).  Level 0 alone (~3.7 k waves at 2^20) fills the chip's
+// 3 x 1024 wave slots 1.2 rounds deep and ran at ~0.7 of the issue rate on the
+// batch's critical path; inside the accumulation's grid its waves share the
+// dispatch with ~15 k accumulation waves and the last round's idle slots fill
+// with accumulation work.  Registers: the larger of the two bodies (149), still
+// 3 waves per SIMD.
+template <class PT>
+static __global__ void __launch_bounds__(256, MSM_ACC_WAVES)
+    k_accumulate_l0(const AccSched S, const PT *__restrict__ pts, Xyzz<Fp> *__restrict__ buckets, size_t nbuckets,
+                    const Xyzz<Fp> *__restrict__ l0src, const uint32_t *__restrict__ l0idx,
+                    const uint32_t *__restrict__ l0starts, Xyzz<Fp> *__restrict__ l0dst, size_t l0out,
+                    uint32_t l0blocks, int l0_last) {
+  // l0_last: level-0 workgroups after the accumulation's instead of before
+  const uint32_t nacc = gridDim.x - l0blocks;
+  const bool l0 = l0_last ? blockIdx.x >= nacc : blockIdx.x < l0blocks;
+  const uint32_t b = l0 ? (l0_last ? blockIdx.x - nacc : blockIdx.x) : (l0_last ? blockIdx.x : blockIdx.x - l0blocks);
+  const size_t t = (size_t)b * blockDim.x + threadIdx.x;
+  if (l0) {
+    if (t < l0out) segsum_one<1>(l0src, l0idx, l0starts, l0dst, t);
+  } else if (t < nbuckets) {
+    accumulate_bucket<1>(S, pts, buckets, t);
+  }
 }
 
 // ------------------------------------------------------- dense scan reduce --

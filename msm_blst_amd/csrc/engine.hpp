@@ -217,6 +217,14 @@ class WeightedReducer {
   // launch beside an accumulation costs it time).
   void ensure_group(int set, int nmsm);
   void launch_head_slot(hipStream_t s, const void *S, int set, int slot);
+  // the operands launch_head_slot would pass to its k_segsum (level 0 into slot
+  // `slot` of set `set`), for a caller that runs level 0 inside another grid
+  struct HeadArgs {
+    const uint32_t *idx, *starts;
+    void *dst;
+    size_t nout;
+  };
+  HeadArgs head_args(int set, int slot);
   void launch_tail_group(hipStream_t s, int set, int nmsm);          // levels >= 1, dense, finalize
   void copy_out_group(hipStream_t s, int set, int nmsm, void *host);  // nmsm * out_bytes()
 
@@ -426,6 +434,10 @@ class Ches {
   // accumulation of scalar set r of front set `set` into bucket set bset
   // (table: the table_ of this engine, or of a segment's engine in run_jobs)
   void accumulate(hipStream_t s, int set, int r, int bset, const void *table = nullptr);
+  // G1 batch: accumulation as above in the same grid as level 0 of the MSM
+  // whose buckets are in l0_bset, into reducer set gset / slot (k_accumulate_l0)
+  void accumulate_l0(hipStream_t s, int set, int r, int bset, const void *table, int l0_bset, int gset, int slot,
+                     int l0_last);
 };
 
 // BGMW95 fixed-base variant (ref main_p1.cpp:94-122, 294-398;

@@ -280,13 +280,10 @@ struct PayloadStream {
 // entry count, BucketSort) so the 64 lanes of a wave run loops of nearly equal
 // length and the longest buckets start first.  Everything is read by schedule
 // position (AccSched: coalesced); S.order[t] is the bucket the sum is stored to.
-template <int G, class PT = Aff<typename FieldOf<G>::F>>
-__global__ void __launch_bounds__(256, MSM_ACC_WAVES)
-    k_accumulate(const AccSched S, const PT *__restrict__ pts, Xyzz<typename FieldOf<G>::F> *__restrict__ buckets,
-                 size_t nbuckets) {
+template <int G, class PT>
+__device__ __forceinline__ void accumulate_bucket(const AccSched &S, const PT *__restrict__ pts,
+                                                  Xyzz<typename FieldOf<G>::F> *__restrict__ buckets, size_t t) {
   typedef typename FieldOf<G>::F F;
-  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nbuckets) return;
   const uint32_t cnt = S.counts[t];
   const PayloadStream ps(S, (uint32_t)t);
   Xyzz<F> acc;
@@ -298,6 +295,13 @@ __global__ void __launch_bounds__(256, MSM_ACC_WAVES)
     xyzz_madd(acc, p, (e >> 31) != 0);
   }
   st16(&buckets[S.order[t]], acc);
+}
+template <int G, class PT = Aff<typename FieldOf<G>::F>>
+__global__ void __launch_bounds__(256, MSM_ACC_WAVES)
+    k_accumulate(const AccSched S, const PT *__restrict__ pts, Xyzz<typename FieldOf<G>::F> *__restrict__ buckets,
+                 size_t nbuckets) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < nbuckets) accumulate_bucket<G>(S, pts, buckets, t);
 }
 
 // One level of the bucket reduction.  Invariant per window:
