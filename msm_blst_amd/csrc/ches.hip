@@ -792,20 +792,23 @@ void Ches<G>::accumulate(hipStream_t s, int set, int r, int bset, const void *ta
 template <int G>
 void Ches<G>::accumulate_l0(hipStream_t s, int set, int r, int bset, const void *table, int l0_bset, int gset,
                             int slot, int l0_last) {
-  if constexpr (G != 1) {
-    throw std::runtime_error("accumulate_l0: G1 only");
-  } else {
-    const size_t NB = bucket_count();
-    ChesFrontSet &f = fs_[set];
-    const typename WeightedReducer<G>::HeadArgs a = red_.head_args(gset, slot);
-    const unsigned l0b = (unsigned)((a.nout + 255) / 256), accb = (unsigned)((NB + 255) / 256);
-    hipLaunchKernelGGL((k_accumulate_l0<AffP<Fp>>), dim3(accb + l0b), dim3(256), 0, s,
-                       f.sort.sched(f.order.as<uint32_t>(), f.sorted.as<uint32_t>(), r, NB),
-                       table ? static_cast<const AffP<Fp> *>(table) : table_.as<AffP<Fp>>(), buckets_[bset].as<Xyzz<Fp>>(),
-                       NB, buckets_[l0_bset].as<Xyzz<Fp>>(), a.idx, a.starts, static_cast<Xyzz<Fp> *>(a.dst), a.nout,
-                       l0b, l0_last);
-    MSM_HIP_CHECK(hipGetLastError());
-  }
+  typedef typename FieldOf<G>::F F;
+  const size_t NB = bucket_count();
+  ChesFrontSet &f = fs_[set];
+  const typename WeightedReducer<G>::HeadArgs a = red_.head_args(gset, slot);
+  const AccSched S = f.sort.sched(f.order.as<uint32_t>(), f.sorted.as<uint32_t>(), r, NB);
+  const AffP<F> *T = table ? static_cast<const AffP<F> *>(table) : table_.as<AffP<F>>();
+  // lanes: one per bucket / output (G1), two (G2 lane pairs)
+  const unsigned l0b = (unsigned)((G * a.nout + 255) / 256), accb = (unsigned)((G * NB + 255) / 256);
+  if constexpr (G == 1)
+    hipLaunchKernelGGL((k_accumulate_l0<AffP<F>>), dim3(accb + l0b), dim3(256), 0, s, S, T,
+                       buckets_[bset].as<Xyzz<F>>(), NB, buckets_[l0_bset].as<Xyzz<F>>(), a.idx, a.starts,
+                       static_cast<Xyzz<F> *>(a.dst), a.nout, l0b, l0_last);
+  else
+    hipLaunchKernelGGL((k_accumulate2p_l0<AffP<F>>), dim3(accb + l0b), dim3(256), 0, s, S, T,
+                       buckets_[bset].as<Xyzz<F>>(), NB, buckets_[l0_bset].as<Xyzz<F>>(), a.idx, a.starts,
+                       static_cast<Xyzz<F> *>(a.dst), a.nout, l0b, l0_last);
+  MSM_HIP_CHECK(hipGetLastError());
 }
 
 template <int G>
@@ -1109,8 +1112,8 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
       }
     }
   }
-  // Level 0 inside the next accumulation's grid (G1, MSM_L0_FUSE=1: its
-  // workgroups first, =2: last; k_accumulate_l0): MSM k's launch also runs
+  // Level 0 inside the next accumulation's grid (MSM_L0_FUSE=1: its
+  // workgroups first, =2: last; k_accumulate_l0 / k_accumulate2p_l0): MSM k's launch also runs
   // level 0 of MSM k - 1 on the caller's stream, the last MSM's level 0 runs
   // alone after the loop, and reducer set q % 2 is reused by group q + 2 only
   // after tail q (event evt[q]: level 0 no longer runs on the tail's stream).
@@ -1118,7 +1121,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
     const char *e = getenv("MSM_L0_FUSE");
     return e ? std::max(0, std::min(2, atoi(e))) : 0;
   }();
-  const int fuse = G == 1 && nl < 2 ? fuse_env : 0;
+  const int fuse = nl < 2 ? fuse_env : 0;
   auto l0_group_tail = [&](size_t p) {  // after level 0 of MSM p (recorded as evh[p] on s)
     const size_t pq = p / R, pslot = p % R;
     if (pslot + 1 != R && p + 1 != count) return;

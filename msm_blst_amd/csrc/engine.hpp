@@ -434,8 +434,8 @@ class Ches {
   // accumulation of scalar set r of front set `set` into bucket set bset
   // (table: the table_ of this engine, or of a segment's engine in run_jobs)
   void accumulate(hipStream_t s, int set, int r, int bset, const void *table = nullptr);
-  // G1 batch: accumulation as above in the same grid as level 0 of the MSM
-  // whose buckets are in l0_bset, into reducer set gset / slot (k_accumulate_l0)
+  // batch: accumulation as above in the same grid as level 0 of the MSM whose
+  // buckets are in l0_bset, into reducer set gset / slot (k_accumulate_l0)
   void accumulate_l0(hipStream_t s, int set, int r, int bset, const void *table, int l0_bset, int gset, int slot,
                      int l0_last);
 };

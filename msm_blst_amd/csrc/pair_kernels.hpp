@@ -149,10 +149,8 @@ static __global__ void __launch_bounds__(128)
 
 // k_accumulate (kernels.hpp) for G2 with two lanes per bucket
 template <class PT>
-__global__ void __launch_bounds__(256)
-    k_accumulate2p(const AccSched S, const PT *__restrict__ pts, Xyzz<Fp2> *__restrict__ buckets, size_t nbuckets) {
-  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= 2 * nbuckets) return;  // whole pairs only: 2 nbuckets lanes
+__device__ __forceinline__ void accumulate_pair(const AccSched &S, const PT *__restrict__ pts,
+                                                Xyzz<Fp2> *__restrict__ buckets, size_t t) {
   const int comp = (int)(t & 1);
   const uint32_t pos = (uint32_t)(t >> 1);  // schedule position (k_accumulate)
   const uint32_t cnt = S.counts[pos];
@@ -168,15 +166,17 @@ __global__ void __launch_bounds__(256)
   }
   st_xyzz2l(&buckets[S.order[pos]], acc, comp);
 }
+template <class PT>
+__global__ void __launch_bounds__(256)
+    k_accumulate2p(const AccSched S, const PT *__restrict__ pts, Xyzz<Fp2> *__restrict__ buckets, size_t nbuckets) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < 2 * nbuckets) accumulate_pair(S, pts, buckets, t);  // whole pairs only: 2 nbuckets lanes
+}
 
 // k_segsum (ches_kernels.hpp) for G2 with two lanes per output
-static __global__ void __launch_bounds__(256)
-    k_segsum2p(const Xyzz<Fp2> *__restrict__ src, const uint32_t *__restrict__ idx, const uint32_t *__restrict__ starts,
-               Xyzz<Fp2> *__restrict__ dst, size_t nout, size_t src_stride, size_t dst_stride) {
-  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= 2 * nout) return;
-  src += blockIdx.y * src_stride;  // MSM blockIdx.y of a batch group (k_segsum)
-  dst += blockIdx.y * dst_stride;
+__device__ __forceinline__ void segsum_pair(const Xyzz<Fp2> *__restrict__ src, const uint32_t *__restrict__ idx,
+                                            const uint32_t *__restrict__ starts, Xyzz<Fp2> *__restrict__ dst,
+                                            size_t t) {
   const int comp = (int)(t & 1);
   const size_t o = t >> 1;
   const uint32_t lo = starts[o], hi = starts[o + 1];
@@ -202,6 +202,32 @@ static __global__ void __launch_bounds__(256)
 #endif
   }
   st_xyzz2l(&dst[o], acc, comp);
+}
+static __global__ void __launch_bounds__(256)
+    k_segsum2p(const Xyzz<Fp2> *__restrict__ src, const uint32_t *__restrict__ idx, const uint32_t *__restrict__ starts,
+               Xyzz<Fp2> *__restrict__ dst, size_t nout, size_t src_stride, size_t dst_stride) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 2 * nout) return;
+  // MSM blockIdx.y of a batch group (k_segsum)
+  segsum_pair(src + blockIdx.y * src_stride, idx, starts, dst + blockIdx.y * dst_stride, t);
+}
+// k_accumulate_l0 (ches_kernels.hpp) for G2: level 0 of the previous MSM and
+// this MSM's accumulation in one grid, both on lane pairs
+template <class PT>
+__global__ void __launch_bounds__(256)
+    k_accumulate2p_l0(const AccSched S, const PT *__restrict__ pts, Xyzz<Fp2> *__restrict__ buckets, size_t nbuckets,
+                      const Xyzz<Fp2> *__restrict__ l0src, const uint32_t *__restrict__ l0idx,
+                      const uint32_t *__restrict__ l0starts, Xyzz<Fp2> *__restrict__ l0dst, size_t l0out,
+                      uint32_t l0blocks, int l0_last) {
+  const uint32_t nacc = gridDim.x - l0blocks;
+  const bool l0 = l0_last ? blockIdx.x >= nacc : blockIdx.x < l0blocks;
+  const uint32_t b = l0 ? (l0_last ? blockIdx.x - nacc : blockIdx.x) : (l0_last ? blockIdx.x : blockIdx.x - l0blocks);
+  const size_t t = (size_t)b * blockDim.x + threadIdx.x;
+  if (l0) {
+    if (t < 2 * l0out) segsum_pair(l0src, l0idx, l0starts, l0dst, t);
+  } else if (t < 2 * nbuckets) {
+    accumulate_pair(S, pts, buckets, t);
+  }
 }
 
 // k_suffix_step / k_pair_step (ches_kernels.hpp) for G2 with two lanes per output

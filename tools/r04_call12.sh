@@ -8,7 +8,7 @@ O=$R/gpurun_out/${1:-r04l}
 mkdir -p $O
 export TMPDIR=/tmp
 echo "start $(date +%T)"
-MSM_L0_FUSE=1 timeout -k 10 400 python3 -u -m pytest tests/test_gpu_ches.py tests/test_gpu_multi.py -m gpu -v --timeout 200 --timeout-method thread > $O/pytest_fuse1.txt 2>&1
+MSM_L0_FUSE=1 timeout -k 10 400 python3 -u -m pytest tests/test_gpu_ches.py tests/test_gpu_multi.py tests/test_gpu_parity.py -m gpu -v --timeout 200 --timeout-method thread > $O/pytest_fuse1.txt 2>&1
 rc=$?; echo "pytest fuse1 rc=$rc $(date +%T) $(tail -1 $O/pytest_fuse1.txt)"; grep -E "FAILED|^E " $O/pytest_fuse1.txt | head -20
 [ $rc -eq 0 ] || exit 1
 run() {  # label, env...
@@ -20,5 +20,10 @@ for i in 1 2; do
   run base$i MSM_L0_FUSE=0
   run fuse1_$i MSM_L0_FUSE=1
   run fuse2_$i MSM_L0_FUSE=2
+  run freehi$i MSM_L0_FUSE=0 MSM_ACC_AFTER_L0=0 MSM_TAIL_PRIO=1
+done
+for F in 0 1; do
+  MSM_L0_FUSE=$F timeout -k 10 400 python3 -u bench.py --group 2 --no-configs --no-cpu-baseline --no-compare > $O/g2_f$F.json 2> $O/g2_f$F.err || exit 1
+  python3 -c "import json; d=json.load(open('$O/g2_f$F.json')); print('G2 fuse $F', d['value'], d['ms_per_step'], d['roofline']['kernel_ms'], d['parity_vs_reference'])"
 done
 echo "done $(date +%T)"
