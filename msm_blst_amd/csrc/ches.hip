@@ -1112,8 +1112,10 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
       }
     }
   }
-  // Level 0 inside the next accumulation's grid (MSM_L0_FUSE=1: its
-  // workgroups first, =2: last; k_accumulate_l0 / k_accumulate2p_l0): MSM k's launch also runs
+  // Level 0 inside the next accumulation's grid (A/B knob, off by default:
+  // measured slower, resident 434-438 vs 446-450 M pairs/s, G2 164.4 vs 165.3 M,
+  // profiles/r04_l0_fuse_ab.txt; MSM_L0_FUSE=1: level-0 workgroups first, =2:
+  // last; k_accumulate_l0 / k_accumulate2p_l0): MSM k's launch also runs
   // level 0 of MSM k - 1 on the caller's stream, the last MSM's level 0 runs
   // alone after the loop, and reducer set q % 2 is reused by group q + 2 only
   // after tail q (event evt[q]: level 0 no longer runs on the tail's stream).
