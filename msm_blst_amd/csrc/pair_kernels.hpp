@@ -203,7 +203,10 @@ __device__ __forceinline__ void segsum_pair(const Xyzz<Fp2> *__restrict__ src, c
   }
   st_xyzz2l(&dst[o], acc, comp);
 }
-static __global__ void __launch_bounds__(256)
+#ifndef MSM_SEGSUM2P_WAVES
+#define MSM_SEGSUM2P_WAVES 2
+#endif
+static __global__ void __launch_bounds__(256, MSM_SEGSUM2P_WAVES)
     k_segsum2p(const Xyzz<Fp2> *__restrict__ src, const uint32_t *__restrict__ idx, const uint32_t *__restrict__ starts,
                Xyzz<Fp2> *__restrict__ dst, size_t nout, size_t src_stride, size_t dst_stride) {
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;

@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--log-n", type=int, default=20)
     ap.add_argument("--label", default=os.environ.get("AB_LABEL", ""))
     ap.add_argument("--profiling", type=int, default=0, help="ctx.set_profiling (bench.py turns it on)")
+    ap.add_argument("--pre", type=int, default=0, help="an untimed batch of this many sets after the warm-up")
+    ap.add_argument("--pre-h2d", type=int, default=0, help="the --pre batch from host memory (else resident)")
     a = ap.parse_args()
     import torch
     import msm_blst_amd as m
@@ -48,6 +50,9 @@ def main():
         return n * K / (time.perf_counter() - t), r
 
     ctx.mult_batch(host.data_ptr(), min(W, K), 32, set_stride=SS, on_device=False, stream=sp)
+    if a.pre:
+        ctx.mult_batch(host.data_ptr() if a.pre_h2d else d_all.data_ptr(), min(a.pre, K), 32, set_stride=SS,
+                       on_device=not a.pre_h2d, stream=sp)
     h2d, res, ref = [], [], None
     for i in range(a.reps):
         v, r = timed(host.data_ptr(), False)
