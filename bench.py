@@ -155,6 +155,11 @@ def main():
     ap.add_argument("--no-batch", action="store_true",
                     help="CHES: time K independent synchronous MSMs instead of one pipelined batch of K")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--setup-batch", type=int, choices=(0, 1), default=1,
+                    help="CHES batch: the context's setup ends with one untimed pipelined batch over the K resident "
+                         "sets (sizes and primes every batch buffer, stream and reducer set: the engine's steady "
+                         "state), before the W warm-up steps; the first timed batch after a 3-5 set warm-up alone "
+                         "measured 1-3 %% below later ones (profiles/r04_first_batch_ab.txt)")
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the other BASELINE configs' legs (configs[0], [1], [4], the blst drop-in at 2^20)")
     ap.add_argument("--cpu-sample-log-n", type=int, default=20)
@@ -266,10 +271,9 @@ def main():
     batched = args.method == "ches" and not args.no_batch
     legs = {}
     if batched:
-        pre = float(os.environ.get("BENCH_PREHEAT_MS", "0"))  # study knob: untimed sync MSMs before the warmup
-        t_pre = time.perf_counter()
-        while (time.perf_counter() - t_pre) * 1e3 < pre:
-            mult(0)
+        if args.setup_batch:  # part of the context's setup, before the W warm-up steps (see --setup-batch)
+            ctx.mult_batch(dptr, K, 32, set_stride=SS, on_device=True, stream=sp)
+            torch.cuda.synchronize(dev)
         if W:
             ctx.mult_batch(hptr, min(W, K), 32, set_stride=SS, on_device=False, stream=sp)
         with Bracket(world, dev, xdev) as b:  # headline: host scalars, H2D inside the pipeline
@@ -458,6 +462,7 @@ def main():
         "phases_ms": {k: round(v, 4) for k, v in phases.items()},
         "phases_note": "one synchronous MSM (profiled) after the timed region" if batched else "last timed step",
         "pipelined_batch": batched,
+        "setup_batch": bool(batched and args.setup_batch),
         "parity_vs_reference": parity,
         "parity_detail": {"set0_vs_golden": golden_ok, "batch_equals_sync_all_sets": batch_eq_sync,
                           "pippenger_cross_check_all_ranks": cross},
