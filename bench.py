@@ -155,11 +155,10 @@ def main():
     ap.add_argument("--no-batch", action="store_true",
                     help="CHES: time K independent synchronous MSMs instead of one pipelined batch of K")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--setup-batch", type=int, choices=(0, 1), default=1,
-                    help="CHES batch: the context's setup ends with one untimed pipelined batch over the K resident "
-                         "sets (sizes and primes every batch buffer, stream and reducer set: the engine's steady "
-                         "state), before the W warm-up steps; the first timed batch after a 3-5 set warm-up alone "
-                         "measured 1-3 %% below later ones (profiles/r04_first_batch_ab.txt)")
+    ap.add_argument("--setup-batch", type=int, choices=(0, 1), default=0,
+                    help="study knob: the context's setup ends with one untimed pipelined batch over the K resident "
+                         "sets, before the W warm-up steps (measured no effect on the first timed batch, "
+                         "profiles/r04_setup_batch_ab.txt)")
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the other BASELINE configs' legs (configs[0], [1], [4], the blst drop-in at 2^20)")
     ap.add_argument("--cpu-sample-log-n", type=int, default=20)
