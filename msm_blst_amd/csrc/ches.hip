@@ -1041,6 +1041,10 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
                                    cstream_));
     MSM_HIP_CHECK(hipEventRecord(evc[g], cstream_));
   };
+  static const bool front_after_l0 = [] {
+    const char *e = getenv("MSM_FRONT_AFTER_L0");
+    return e && atoi(e) != 0;
+  }();
   auto front_group = [&](size_t g) {
     if (g >= nfg) return;
     const bool copied = scalars_on_host && !zero_copy;
@@ -1048,6 +1052,9 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
     if (g >= (size_t)nfr) {  // front set g % nfr: every accumulation of group g - nfr has read it
       const size_t last = fgb[g - nfr + 1] - 1;
       MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, eva[last], 0));
+      // A/B knob: also after that MSM's level 0, so the front starts beside the
+      // next accumulation instead of beside level 0 (one-lane schedule)
+      if (front_after_l0 && nl < 2) MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, evh[last], 0));
       for (size_t d = 1; d < (size_t)nl && last >= d && last - d >= fgb[g - nfr]; ++d)  // its other lanes
         MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, eva[last - d], 0));
     }
