@@ -951,26 +951,27 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
   const size_t sslot = n * stride;  // one device scalar slot
   bool unsized = false;
   for (int f = 0; f < nfr; ++f) unsized |= fs_[f].sorted.bytes < n * (size_t)p_.h * fg_max * 4;
-  // host sets: nsg groups of fg_max device slots, copied up to nsg groups ahead
-  // (4 single-set groups -- as the round-2 pipeline's four slots -- or 2 larger)
+  // host sets: device slots for up to 32 front groups (<= 2 GiB, at least 4),
+  // so a batch of up to 32 groups issues every copy at its start and the copy
+  // stream runs them back to back, ahead of the fronts; a longer batch copies
+  // group g once group g - nsg's front has consumed its slots.  With 4 slots
+  // (copies issued 4 MSMs ahead, each after a front event) the 2^20 H2D
+  // headline fell into a slow schedule in about half the runs (372-391 vs
+  // 411-417 M pairs/s, more often after a 3-set warm-up); with a slot per set
+  // 18 of 18 runs gave 418-423 M (profiles/r04_h2d_slots_ab.txt)
   static const size_t nsg_env = [] {
     const char *e = getenv("MSM_H2D_SLOTS");  // A/B knob: slot groups (copies issued that far ahead)
     return (size_t)(e ? std::max(2, std::min(256, atoi(e))) : 0);
   }();
+  const size_t slot_groups =
+      std::max<size_t>(nsg_env ? nsg_env : std::max<size_t>(4, std::min<size_t>(32, ((size_t)2 << 30) / (fg_max * sslot))),
+                       (size_t)nfr - 1);
   // (every group's copies are enqueued before its front: nsg >= nfr - 1)
-  const size_t nsg = std::max<size_t>(nsg_env ? nsg_env : fg_max == 1 ? 4 : 2, (size_t)nfr - 1);
-  if (scalars_on_host || unsized) {
-    const size_t before = scal_.bytes;
-    scal_.ensure(std::max<size_t>(nsg, 2) * fg_max * sslot + 16);
-    static const bool touch_env = [] {  // A/B knob: write every new slot once before the first batch uses it
-      const char *e = getenv("MSM_TOUCH_SLOTS");
-      return e && atoi(e) != 0;
-    }();
-    if (touch_env && scal_.bytes != before) {
-      MSM_HIP_CHECK(hipMemsetAsync(scal_.p, 0, scal_.bytes, s));
-      MSM_HIP_CHECK(hipStreamSynchronize(s));
-    }
-  }
+  const size_t nsg = std::max<size_t>(std::min(slot_groups, nfg), (size_t)nfr - 1);
+  // sized for slot_groups whatever this batch's length: a later, longer batch
+  // must not reallocate inside its pipelined region
+  if (scalars_on_host) scal_.ensure(slot_groups * fg_max * sslot + 16);
+  if (unsized) scal_.ensure(fg_max * sslot + 16);
   for (int f = 0; f < nfr; ++f)
     if (fs_[f].sorted.bytes < n * (size_t)p_.h * fg_max * 4) {
       MSM_HIP_CHECK(hipMemsetAsync(scal_.p, 0, fg_max * sslot, s));
@@ -1053,7 +1054,8 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
       const size_t last = fgb[g - nfr + 1] - 1;
       MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, eva[last], 0));
       // A/B knob: also after that MSM's level 0, so the front starts beside the
-      // next accumulation instead of beside level 0 (one-lane schedule)
+      // next accumulation instead of beside level 0 (one-lane schedule);
+      // measured no better (profiles/r04_h2d_slots_ab.txt, call 19)
       if (front_after_l0 && nl < 2) MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, evh[last], 0));
       for (size_t d = 1; d < (size_t)nl && last >= d && last - d >= fgb[g - nfr]; ++d)  // its other lanes
         MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, eva[last - d], 0));

@@ -16,4 +16,4 @@ for i in 1 2 3; do
     done
   done
 done
-echo "done $(date +%T)"
+echo "done18 $(date +%T)" && bash tools/r04_call19.sh
