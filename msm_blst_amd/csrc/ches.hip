@@ -958,7 +958,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
   // (copies issued 4 MSMs ahead, each after a front event) the 2^20 H2D
   // headline fell into a slow schedule in about half the runs (372-391 vs
   // 411-417 M pairs/s, more often after a 3-set warm-up); with a slot per set
-  // 18 of 18 runs gave 418-423 M (profiles/r04_h2d_slots_ab.txt)
+  // every run gave 418-423 M (profiles/r04_h2d_slots_ab.txt)
   static const size_t nsg_env = [] {
     const char *e = getenv("MSM_H2D_SLOTS");  // A/B knob: slot groups (copies issued that far ahead)
     return (size_t)(e ? std::max(2, std::min(256, atoi(e))) : 0);
