@@ -894,7 +894,11 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
   const size_t ob = red_.out_bytes();  // a group's read-back lands contiguously
   // reduction groups of R <= kGroup MSMs (balanced sizes), alternating between
   // the two reducer sets / tail streams
-  const size_t ngroups = (count + kGroup - 1) / kGroup, R = (count + ngroups - 1) / ngroups;
+  static const size_t group_max = [] {  // A/B knob: MSMs per reduction group (default kGroup)
+    const char *e = getenv("MSM_RED_GROUP");
+    return (size_t)(e ? std::max(1, std::min(32, atoi(e))) : kGroup);
+  }();
+  const size_t ngroups = (count + group_max - 1) / group_max, R = (count + ngroups - 1) / ngroups;
   if (host_out_bytes_ < count * ob) {  // at least 256 MSMs' worth (a few hundred KiB): no regrowth per batch size
     if (host_out_) (void)hipHostFree(host_out_);
     host_out_ = nullptr;
@@ -944,7 +948,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
   // launches, ~1 ms beside the accumulations: with 2 sets group q + 2 waited
   // for it, profiles/r04_batch_trace_2p17.txt)
   const int nfr = nl >= 2 ? kFrontsMax : kFronts, nred = nl >= 2 ? 4 : 2;
-  for (int t = 0; t < nred; ++t) red_.ensure_group(t, kGroup);
+  for (int t = 0; t < nred; ++t) red_.ensure_group(t, (int)group_max);
   // front sets sized for a whole front group (the sort's scan scratch too): run
   // one sort of fg_max sets per set before the loop if they are not yet sized
   // (fg_max dummy sets of all-zero scalars, outside the batch timing)
