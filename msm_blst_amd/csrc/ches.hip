@@ -343,6 +343,8 @@ void WeightedReducer<G>::plan(const std::vector<uint32_t> &w, const std::vector<
   maxp_ = 1;
   for (size_t l = 0; l + 1 < nout_.size(); ++l) maxp_ = std::max(maxp_, nout_[l]);
   for (size_t l = 0; l + 1 < bnout_.size(); ++l) maxp_ = std::max(maxp_, bnout_[l]);  // bit phase levels
+  maxp1_ = 1;  // batch group tails: level l writes part_[l & 1]; the odd levels are at most half of level 0
+  for (size_t l = 1; l + 1 < nout_.size(); l += 2) maxp1_ = std::max(maxp1_, nout_[l]);
   for (int st = 0; st < NSETS; ++st) {  // a new plan: sets are (re)sized on their next use
     part_[st][0].release();
     part_[st][1].release();
@@ -423,7 +425,7 @@ void WeightedReducer<G>::ensure_group(int set, int nmsm) {
   typedef typename FieldOf<G>::F F;
   if (set < 0 || set >= NSETS || nmsm < 1) throw std::runtime_error("WeightedReducer: bad group");
   part_[set][0].ensure((size_t)nmsm * maxp_ * sizeof(Xyzz<F>));
-  part_[set][1].ensure((size_t)nmsm * maxp_ * sizeof(Xyzz<F>));
+  part_[set][1].ensure((size_t)nmsm * maxp1_ * sizeof(Xyzz<F>));
   dense_buf_[set].ensure((size_t)nmsm * dense_slots() * sizeof(Xyzz<F>));
   const size_t NT = (size_t)nmsm * dense_slots();  // ScanReducer::launch's buffers for W = 2 nwin nmsm
   dense_[set].buf[0].ensure(NT * sizeof(Xyzz<F>));
@@ -459,7 +461,9 @@ void WeightedReducer<G>::launch_tail_group(hipStream_t s, int set, int nmsm) {
     const bool last = l + 1 == L;
     Xyzz<F> *dst = last ? dense_buf_[set].as<Xyzz<F>>() : part_[set][l & 1].as<Xyzz<F>>();
     const uint32_t *ix = last ? idx_.as<uint32_t>() + final_perm_off_ : nullptr;
-    launch_segsum<G>(s, src, ix, starts_[l].as<uint32_t>(), dst, nout_[l], nmsm, maxp_, last ? dense_slots() : maxp_);
+    const size_t sstride = (l & 1) ? maxp_ : maxp1_;  // level l - 1 wrote part_[(l - 1) & 1]
+    launch_segsum<G>(s, src, ix, starts_[l].as<uint32_t>(), dst, nout_[l], nmsm, sstride,
+                     last ? dense_slots() : (l & 1) ? maxp1_ : maxp_);
     MSM_HIP_CHECK(hipGetLastError());
     src = dst;
   }

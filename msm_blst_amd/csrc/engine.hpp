@@ -232,6 +232,7 @@ class WeightedReducer {
   size_t dense_slots() const { return (size_t)2 * nwin_ << sbits_; }
   size_t bit_slots() const { return (size_t)2 * nwin_ * sbits_; }
   size_t bsize_ = 0, final_perm_off_ = 0, maxp_ = 1;
+  size_t maxp1_ = 1;  // batch groups: partials per MSM in part_[.][1] (the odd tail levels)
   int sbits_ = 1, nwin_ = 1;
   DevBuf idx_, dense_buf_[NSETS], part_[NSETS][2];
   std::vector<DevBuf> starts_;
@@ -407,7 +408,11 @@ class Ches {
   // groups of 8 vs 2.26-2.27 with groups of 1), so the default group is one
   // MSM; MSM_FRONT_GROUP=<2..8> selects larger groups.  The synchronous MSM uses
   // set 0 with one scalar set.
-  static constexpr int kGroup = 8;       // batch: MSMs per reduction group (WeightedReducer::launch_tail_group)
+  // batch: MSMs per reduction group (WeightedReducer::launch_tail_group).  20:
+  // a batch of up to 20 runs one tail, after its last accumulation, instead of
+  // tails beside accumulations (each costs the one beside it ~0.3 ms); 20 vs
+  // 8 measured +1.2 % (profiles/r04_red_group_ab.txt).  MSM_RED_GROUP overrides.
+  static constexpr int kGroup = 20;
   static constexpr int kFrontGroup = 8;  // batch: largest front group (ramping up 1, 1, 2, 4, 8)
   static constexpr int kFrontGroupDefault = 1;
   // front k+1 may start when accumulation k-2 ends (slack for the copies); the
