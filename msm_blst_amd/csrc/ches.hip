@@ -601,8 +601,8 @@ void Ches<G>::plan_buckets(size_t n) {
   red_.plan(w);
 }
 
-// Accumulation lanes of a batch (run_batch): 2 when one accumulation's lanes
-// (one per bucket for G1, two for G2) fill fewer than ~3 rounds of the chip's
+// Accumulation lanes of a batch (run_batch): 3 (G1) or 2 (G2) when one
+// accumulation's lanes (one per bucket for G1, two for G2) fill fewer than ~3 rounds of the chip's
 // wave slots (1024 SIMDs x the kernel's waves per SIMD x 64 lanes: 3 for
 // k_accumulate<1>, 2 for k_accumulate2p), else 1.  MSM_BATCH_LANES=1|2|3
 // overrides.
@@ -613,8 +613,11 @@ int Ches<G>::batch_lanes() const {
     return e ? std::max(1, std::min(3, atoi(e))) : 0;
   }();
   if (env) return env;
+  // G1 small MSMs take three lanes since round 4's single reduction group per
+  // batch (2^17 / 2^18 / 2^19 batches 0.52 / 0.86 / 1.40 -> 0.49 / 0.80 / 1.35
+  // ms per MSM, profiles/r04_small_lanes_ab.txt); G2 keeps two (not measured)
   const size_t lanes = bucket_count() * (G == 2 ? 2 : 1);
-  return lanes < (size_t)3 * (G == 2 ? 2 : 3) * 1024 * 64 ? 2 : 1;
+  return lanes < (size_t)3 * (G == 2 ? 2 : 3) * 1024 * 64 ? (G == 1 ? 3 : 2) : 1;
 }
 
 template <int G>
@@ -912,9 +915,11 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
     host_out_bytes_ = bytes;
   }
   // (group size cap: kFrontGroupDefault, or MSM_FRONT_GROUP=<1..8>; engine.hpp)
-  // (small MSMs on lanes: groups of 2 -- half the front launches, measured
-  // 0.551 -> 0.530 ms per 2^17 MSM and 0.874 -> 0.845 at 2^18; the 2^20 batch
-  // keeps 1, its wider fronts starve the accumulation, r03_front_group_ab.txt)
+  // (small MSMs on lanes: groups of 2 on two lanes -- half the front launches,
+  // measured 0.551 -> 0.530 ms per 2^17 MSM and 0.874 -> 0.845 at 2^18 -- and 4
+  // on three lanes (profiles/r04_small_lanes_ab.txt); the 2^20 batch keeps 1,
+  // its wider fronts starve the accumulation, r03_front_group_ab.txt and
+  // r04_front_group_ab.txt)
   static const size_t fg_env = [] {
     const char *e = getenv("MSM_FRONT_GROUP");
     return e ? (size_t)std::min(kFrontGroup, std::max(1, atoi(e))) : (size_t)0;
@@ -928,7 +933,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
     const char *e = getenv("MSM_FINE_BT");
     return e && atoi(e) == 256 ? 256 : 1024;
   }();
-  const size_t fg_max = !packed ? 1 : fg_env ? fg_env : nl >= 2 ? 2 : (size_t)kFrontGroupDefault;
+  const size_t fg_max = !packed ? 1 : fg_env ? fg_env : nl >= 3 ? 4 : nl == 2 ? 2 : (size_t)kFrontGroupDefault;
   // front groups of 1, 1, 2, 4, then fg_max MSMs: the first accumulation
   // starts after one front, and each group's host sets (copied while the earlier
   // groups accumulate: a set copies in ~0.6 ms, an MSM accumulates in ~2.3) are
