@@ -291,7 +291,11 @@ void Pippenger<G>::run_batch(hipStream_t s, const uint8_t *d_scalars, size_t str
     MSM_HIP_CHECK(hipStreamCreateWithFlags(&tstream_, hipStreamNonBlocking));
   }
   // groups of R <= kGroup MSMs share one reduction tail (WeightedReducer batch groups)
-  const size_t ngroups = (count + kGroup - 1) / kGroup, R = (count + ngroups - 1) / ngroups;
+  static const size_t group_max = [] {  // A/B knob: MSMs per reduction group
+    const char *e = getenv("MSM_PIP_GROUP");
+    return (size_t)(e ? std::max(1, std::min(32, atoi(e))) : kGroup);
+  }();
+  const size_t ngroups = (count + group_max - 1) / group_max, R = (count + ngroups - 1) / ngroups;
   const size_t ob = red_.out_bytes();
   if (host_out_bytes_ < count * ob) {
     if (host_out_) (void)hipHostFree(host_out_);
@@ -304,7 +308,7 @@ void Pippenger<G>::run_batch(hipStream_t s, const uint8_t *d_scalars, size_t str
   // every buffer the pipeline touches exists before its first launch (an
   // allocation inside the issue loop would synchronise the device)
   for (DevBuf &b : buckets_) b.ensure(NT * sizeof(Xyzz<F>));
-  for (int t = 0; t < kRedSets; ++t) red_.ensure_group(t, kGroup);
+  for (int t = 0; t < kRedSets; ++t) red_.ensure_group(t, (int)group_max);
   for (int f = 0; f < kFronts; ++f)
     if (fs_[f].sorted.bytes < (size_t)W * n_ * 4 + 64) front(s, d_scalars, stride, nbits, nullptr, fs_[f]);
   MSM_HIP_CHECK(hipStreamSynchronize(s));
