@@ -880,7 +880,12 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
     // same priority for both measured equal, tools/batch_sched.py)
     int least = 0, greatest = 0;
     MSM_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    MSM_HIP_CHECK(hipStreamCreateWithPriority(&fstream_, hipStreamNonBlocking, greatest));
+    static const int front_prio = [] {  // A/B knob: 1 greatest (default), 0 normal, -1 least
+      const char *e = getenv("MSM_FRONT_PRIO");
+      return e ? atoi(e) : 1;
+    }();
+    MSM_HIP_CHECK(hipStreamCreateWithPriority(&fstream_, hipStreamNonBlocking,
+                                              front_prio > 0 ? greatest : front_prio < 0 ? least : 0));
     static const bool tail_hi = [] {  // A/B knob: reduction streams at the front's (greatest) priority
       const char *e = getenv("MSM_TAIL_PRIO");
       return e && atoi(e) != 0;
