@@ -25,5 +25,14 @@ python3 $R/tools/roofline_check.py $O/prof.json $O/prof/run_kernel_trace.csv $O/
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python3 $R/bench.py --steps 2 --warmup 0 --no-cpu-baseline --no-compare --no-batch > $O/pmc_fetch.log 2>&1 &&
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- python3 $R/bench.py --steps 2 --warmup 0 --no-cpu-baseline --no-compare --no-batch > $O/pmc_write.log 2>&1 &&
 python3 $R/tools/pmc_traffic.py $O/pmc_fetch/run_counter_collection.csv $O/pmc_write/run_counter_collection.csv ches 20 $O/pmc_traffic.json $R/profiles/r02_gather_cal.json > /dev/null &&
-echo "pmc ok $(date +%T)" && grep accumulate_bytes_per_launch $O/pmc_traffic.json
+echo "pmc ok $(date +%T)" && grep accumulate_bytes_per_launch $O/pmc_traffic.json &&
+cd $R &&
+timeout -k 10 400 python3 -u bench.py --group 2 --no-configs --no-cpu-baseline > $O/bench_g2.json 2> $O/bench_g2.err &&
+python3 -c "import json; d=json.load(open('$O/bench_g2.json')); print('G2', d['value'], d['ms_per_step'], d['parity_vs_reference'], d['valu_roofline']['mad_frac'], d['phases_ms'])" &&
+timeout -k 10 400 python3 -u bench.py --multi-context 8 --one-device --steps 10 --warmup 2 --no-cpu-baseline --no-configs --no-compare > $O/mc8.json 2> $O/mc8.err &&
+python3 -c "import json; d=json.load(open('$O/mc8.json')); print('mc8', {k: (v.get('value'), v.get('ms_per_step'), v.get('parity_vs_reference')) for k, v in d['methods'].items() if 'cfg3' in k})" &&
+for N in 2 4 8; do
+  timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node $N --master-addr 127.0.0.1 --master-port $((29560 + N)) bench.py --gpus $N --dist-backend gloo --one-device --steps 10 --warmup 2 --no-cpu-baseline > $O/n$N.json 2> $O/n$N.err || exit 1
+  python3 -c "import json; d=json.loads(open('$O/n$N.json').read().strip().splitlines()[-1]); print('N=$N', d['value'], d['scaling'], d['config']['n_total'], d['parity_vs_reference'])"
+done
 echo "rc=$?"
