@@ -23,6 +23,7 @@
 #include "ches_kernels.hpp"
 #include "coop.hpp"
 #include "engine.hpp"
+#include "hoststage.hpp"
 #include "pair_kernels.hpp"
 
 #ifndef MSM_GROUP
@@ -1223,7 +1224,14 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
   }
   for (int t = 0; t < kBSets; ++t) MSM_HIP_CHECK(hipStreamSynchronize(tails_[t]));
   MSM_HIP_CHECK(hipStreamSynchronize(fstream_));  // three lanes: the group read-backs ran on the front stream
-  for (size_t k = 0; k < count; ++k) outs[k] = red_.combine((const uint8_t *)host_out_ + k * ob)[0];
+  // the per-MSM host Horner (~20 us each) over the host worker threads: with
+  // one reduction group per batch every combine runs after the last tail
+  auto combine_k = [&](size_t k) { outs[k] = red_.combine((const uint8_t *)host_out_ + k * ob)[0]; };
+  if (count >= 4) {
+    WorkerPool::get().parallel_for(count, combine_k);
+  } else {
+    for (size_t k = 0; k < count; ++k) combine_k(k);
+  }
   profile_ = prof;
   if (prof) {  // average accumulation time over the batch (HIP events on stream s)
     float sum = 0;
