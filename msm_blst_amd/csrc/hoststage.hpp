@@ -155,14 +155,6 @@ class HostStager {
   static constexpr size_t kChunk = (size_t)16 << 20;
   static constexpr size_t kMinSlot = (size_t)1 << 20;
   static constexpr size_t kDirect = (size_t)1 << 20;
-  static constexpr size_t kFirst = (size_t)2 << 20;
-  static size_t first_bytes() {  // MSM_STAGE_FIRST_MB=0 (A/B knob): no short first piece
-    static const size_t v = [] {
-      const char *e = getenv("MSM_STAGE_FIRST_MB");
-      return e ? (atoi(e) > 0 ? (size_t)atoi(e) << 20 : ~(size_t)0) : kFirst;
-    }();
-    return v;
-  }
   static constexpr int kSlots = 4;
   HostStager() = default;
   HostStager(const HostStager &) = delete;
@@ -186,13 +178,11 @@ class HostStager {
       slot_ = want;
       for (int k = 0; k < kSlots; ++k) MSM_HIP_CHECK(hipEventCreateWithFlags(&ev_[k], hipEventDisableTiming));
     }
-    // the first piece is short (kFirst): the DMA starts after a 2-MiB host copy
-    // instead of a whole 16-MiB slot's, the later pieces fill whole slots
-    for (size_t off = 0, len = 0; off < bytes; off += len) {
+    for (size_t off = 0; off < bytes; off += slot_) {
       const int k = next_;
       next_ = (next_ + 1) % kSlots;
       if (used_[k]) MSM_HIP_CHECK(hipEventSynchronize(ev_[k]));  // the slot's previous DMA is done
-      len = std::min(off == 0 ? std::min(slot_, first_bytes()) : slot_, bytes - off);
+      const size_t len = std::min(slot_, bytes - off);
       uint8_t *slot = static_cast<uint8_t *>(ring_) + (size_t)k * slot_;
       parallel_memcpy(slot, static_cast<const uint8_t *>(src) + off, len);
       MSM_HIP_CHECK(hipMemcpyAsync(static_cast<uint8_t *>(dst) + off, slot, len, hipMemcpyHostToDevice, s));
