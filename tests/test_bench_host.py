@@ -1,0 +1,36 @@
+"""CPU tests of bench.py's host-side accounting: the per-madd v_mad_u64_u32
+count behind `valu_roofline.mad_frac` is parsed from the committed gfx950 ISA
+counts (tools/isa_report.sh -> profiles/r04_isa_counts.txt) for G1 (Fp ops on
+one lane) and G2 (lane-pair Fp2 ops, both lanes)."""
+import os
+import re
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+import bench  # noqa: E402
+
+ISA = os.path.join(REPO, "profiles", "r04_isa_counts.txt")
+
+
+def _mads(txt, key):
+    return int(re.search(key + r"\w*\n\s+vgpr \d+ scratch \d+ total \d+ v_mad_u64_u32 (\d+)", txt).group(1))
+
+
+def test_mads_per_madd_from_isa_counts():
+    txt = open(ISA).read()
+    mul, sqr, mul2 = (_mads(txt, k) for k in ("k_op_fp_mulP", "k_op_fp_sqr", "k_op_fp_mul2"))
+    g1, src = bench.isa_mads_per_madd(1, ISA)
+    # ec.hpp xyzz_madd: 6 products, 2 squares, 1 fused two-product sum
+    assert g1 == 6 * mul + 2 * sqr + mul2 and src == os.path.basename(ISA)
+    bs, sq2, ms = (_mads(txt, k) for k in ("k_op_g2l_mul_bs", "k_op_g2l_sqr", "k_op_g2l_mul_sub"))
+    g2, _ = bench.isa_mads_per_madd(2, ISA)
+    assert g2 == 2 * (6 * bs + 2 * sq2 + ms)  # per lane, times the lane pair
+    assert 3000 < g1 < 4000 and 2 * g1 < g2 < 4 * g1
+
+
+def test_mads_per_madd_without_counts(tmp_path):
+    missing = str(tmp_path / "none.txt")
+    assert bench.isa_mads_per_madd(1, missing)[0] == 3567  # the round-3 constant
+    assert bench.isa_mads_per_madd(2, missing)[0] is None  # no G2 figure without lane-pair counts
