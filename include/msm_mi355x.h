@@ -283,6 +283,10 @@ int msm_ches_ctx_load_table(msm_ches_ctx *ctx, const char *path);
 int msm_ches_ctx_set_profiling(msm_ches_ctx *ctx, int on);
 int msm_ches_ctx_phase_times(const msm_ches_ctx *ctx, float out[6]);
 size_t msm_ches_ctx_bucket_count(const msm_ches_ctx *ctx);
+/* accumulation lanes msm_ches_ctx_mult_batch runs (first shard's engine): 1 when
+ * one accumulation fills the chip >= 3 wave-slot rounds deep, else 2-3 MSMs
+ * accumulate side by side (MSM_BATCH_LANES overrides); 0 on a NULL ctx */
+int msm_ches_ctx_batch_lanes(const msm_ches_ctx *ctx);
 void msm_ches_ctx_destroy(msm_ches_ctx *ctx);
 
 /* ---- BGMW95 fixed-base method, device-resident precomputed table ----

@@ -68,6 +68,7 @@ def lib():
     L.msm_ches_ctx_phase_times.argtypes = [vp, vp]
     L.msm_ches_ctx_bucket_count.argtypes = [vp]
     L.msm_ches_ctx_bucket_count.restype = sz
+    L.msm_ches_ctx_batch_lanes.argtypes = [vp]
     L.msm_ches_ctx_destroy.argtypes = [vp]
     L.msm_ches_ctx_destroy.restype = None
     L.msm_ches_bucket_set.argtypes = [i32, i32, vp, sz]

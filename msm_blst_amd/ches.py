@@ -131,6 +131,10 @@ class CHESContext:
     def bucket_count(self):
         return lib().msm_ches_ctx_bucket_count(self._ctx)
 
+    def batch_lanes(self):
+        """Accumulation lanes mult_batch runs (1: the one-lane schedule of the 2^20 headline)."""
+        return lib().msm_ches_ctx_batch_lanes(self._ctx)
+
     def set_profiling(self, on=True):
         check(lib().msm_ches_ctx_set_profiling(self._ctx, int(on)))
 

@@ -844,9 +844,11 @@ int msm_ches_ctx_shards(const msm_ches_ctx *ctx) {
 
 #define CHES_DISPATCH(ctx, CALL) ((ctx)->group == 1 ? (ctx)->g1->CALL : (ctx)->g2->CALL)
 
-// several shards take host memory only (each device gets its own slice)
+// several engines take host memory only (each device gets its own slice); shards
+// merged into one engine on one device (multi.hpp) take device memory like a
+// single-device context
 static bool multi_device_arg(const msm_ches_ctx *ctx, int on_device) {
-  return on_device && (ctx->group == 1 ? ctx->g1->nshards() : ctx->g2->nshards()) > 1;
+  return on_device && (ctx->group == 1 ? ctx->g1->engines() : ctx->g2->engines()) > 1;
 }
 
 int msm_ches_ctx_build_table(msm_ches_ctx *ctx, const void *pts, size_t n, int on_device, void *stream) {
@@ -948,6 +950,8 @@ int msm_ches_ctx_phase_times(const msm_ches_ctx *ctx, float out[6]) {
 }
 
 size_t msm_ches_ctx_bucket_count(const msm_ches_ctx *ctx) { return ctx ? CHES_DISPATCH(ctx, front().bucket_count()) : 0; }
+
+int msm_ches_ctx_batch_lanes(const msm_ches_ctx *ctx) { return ctx ? CHES_DISPATCH(ctx, front().batch_lanes()) : 0; }
 
 void msm_ches_ctx_destroy(msm_ches_ctx *ctx) { delete ctx; }
 

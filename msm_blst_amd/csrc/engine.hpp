@@ -380,6 +380,7 @@ class Ches {
   void set_profiling(bool on) { profile_ = on; }
   const PhaseTimes &times() const { return times_; }
   int device() const { return dev_; }
+  int batch_lanes() const;  // accumulation streams of run_batch (1, 2 or 3)
 
  private:
   int dev_;
@@ -391,7 +392,6 @@ class Ches {
   // digit goes to copy i % copies_ of its bucket (copies share the weight B[k])
   int small_ = 0, copies_ = 1;
   void plan_buckets(size_t n);
-  int batch_lanes() const;  // accumulation streams of run_batch (1 or 2)
   bool profile_ = false;
   PhaseTimes times_;
   // bucket sets: MSM k accumulates into set k % kBSets while the reduction of

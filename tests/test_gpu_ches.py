@@ -168,15 +168,14 @@ def test_mult_batch_matches_single(m, golden):
 @pytest.mark.parametrize("group,log_n,K", [(1, 16, 7), (2, 10, 7), (1, 12, 9), (1, 12, 17), (2, 10, 9),
                                            (2, 10, 17)])
 def test_mult_batch_sets_resident_and_pinned(m, group, log_n, K):
-    """Batches longer than every ring (Ches::run_batch: single-set front groups in
-    kFronts = 3 rotating front sets; kBSets = 2 bucket sets; host sets in 4
-    device slots copied on their own stream, cstream_): K distinct sets from
-    device memory and from page-locked host memory (streamed set by set inside
-    the pipeline) equal the synchronous MSMs.  K = 9 and 17 also
-    exceed one reduction group (kGroup = 8): several groups of uneven size R
-    alternate between the two reducer buffer sets / tail streams and read back
-    at their own offsets (test_batch_front_groups_of_eight repeats K = 17 / 9
-    with front groups of 1, 1, 2, 4, 8 straddling them)."""
+    """K distinct sets from device memory and from page-locked host memory
+    (copied set by set inside the pipeline) equal the synchronous MSMs.  These
+    sizes take the small-MSM LANE schedule of Ches::run_jobs (batch_lanes() = 3
+    for G1, 2 for G2: MSMs accumulate side by side on rotating streams and
+    bucket sets, kFrontsMax = 5 front sets, front groups of 1, 1, 2, 4, 4, ...,
+    four reducer sets).  One reduction group holds up to kGroup = 20 MSMs, so
+    these K form one group; the headline's one-lane schedule and batches of
+    more than 20 are test_gpu_batch_one_lane.py."""
     import numpy as np
     import torch
     n = 1 << log_n

@@ -5,7 +5,8 @@ stream) the reference's golden value (tests/golden, written from the
 reference's own blst_p1s_mult_pippenger).  Covers device and host scalar
 sets, G1 and G2, window sizes with a partial top window (bucket copies),
 64-bit scalars (short window plan) and batch lengths that are not a multiple
-of the reduction group (8)."""
+of the plain-Pippenger reduction group (Pippenger::kGroup = 8,
+engine.hpp; the CHES batch groups 20)."""
 import numpy as np
 import pytest
 
