@@ -158,28 +158,30 @@ void ScanReducer<G>::launch(hipStream_t s, const void *Abuf, int W, int S, bool 
   int cur = 0;
   for (int d = 1; d < S; d <<= 1) {  // suffix sums T_k = sum_{b >= k} A_b
     Xyzz<F> *dst = buf[cur].as<Xyzz<F>>();
-    if (G == 2 && coop)  // lane pairs (fp2l.hpp), one add over 4 waves (coop.hpp)
-      hipLaunchKernelGGL(k_suffix_step_c2p, dim3(nblk(NT, 32)), dim3(256), 0, s,
-                         reinterpret_cast<const Xyzz<Fp2> *>(src), reinterpret_cast<Xyzz<Fp2> *>(dst), S, d, W);
-    else if (G == 2)  // lane pairs (fp2l.hpp)
-      hipLaunchKernelGGL(k_suffix_step2p, dim3(nblk(2 * NT, 64)), dim3(64), 0, s,
-                         reinterpret_cast<const Xyzz<Fp2> *>(src), reinterpret_cast<Xyzz<Fp2> *>(dst), S, d, W);
-    else if (coop) hipLaunchKernelGGL(k_suffix_step_c<G>, dim3(nblk(NT, 64)), dim3(256), 0, s, src, dst, S, d, W);
-    else hipLaunchKernelGGL(k_suffix_step<G>, dim3(nblk(NT, 64)), dim3(64), 0, s, src, dst, S, d, W);
+    if constexpr (G == 2) {  // lane pairs (fp2l.hpp); coop: one add over 4 waves (coop.hpp)
+      if (coop)
+        hipLaunchKernelGGL(k_suffix_step_c2p, dim3(nblk(NT, 32)), dim3(256), 0, s, src, dst, S, d, W);
+      else
+        hipLaunchKernelGGL(k_suffix_step2p, dim3(nblk(2 * NT, 64)), dim3(64), 0, s, src, dst, S, d, W);
+    } else {
+      if (coop) hipLaunchKernelGGL(k_suffix_step_c<G>, dim3(nblk(NT, 64)), dim3(256), 0, s, src, dst, S, d, W);
+      else hipLaunchKernelGGL(k_suffix_step<G>, dim3(nblk(NT, 64)), dim3(64), 0, s, src, dst, S, d, W);
+    }
     MSM_HIP_CHECK(hipGetLastError());
     src = dst;
     cur ^= 1;
   }
   for (size_t len = NT; len > (size_t)W; len >>= 1) {  // sum_k T_k = sum_b b A_b
     Xyzz<F> *dst = buf[cur].as<Xyzz<F>>();
-    if (G == 2 && coop)
-      hipLaunchKernelGGL(k_pair_step_c2p, dim3(nblk(len / 2, 32)), dim3(256), 0, s,
-                         reinterpret_cast<const Xyzz<Fp2> *>(src), reinterpret_cast<Xyzz<Fp2> *>(dst), len / 2);
-    else if (G == 2)
-      hipLaunchKernelGGL(k_pair_step2p, dim3(nblk(len, 64)), dim3(64), 0, s,
-                         reinterpret_cast<const Xyzz<Fp2> *>(src), reinterpret_cast<Xyzz<Fp2> *>(dst), len / 2);
-    else if (coop) hipLaunchKernelGGL(k_pair_step_c<G>, dim3(nblk(len / 2, 64)), dim3(256), 0, s, src, dst, len / 2);
-    else hipLaunchKernelGGL(k_pair_step<G>, dim3(nblk(len / 2, 64)), dim3(64), 0, s, src, dst, len / 2);
+    if constexpr (G == 2) {
+      if (coop)
+        hipLaunchKernelGGL(k_pair_step_c2p, dim3(nblk(len / 2, 32)), dim3(256), 0, s, src, dst, len / 2);
+      else
+        hipLaunchKernelGGL(k_pair_step2p, dim3(nblk(len, 64)), dim3(64), 0, s, src, dst, len / 2);
+    } else {
+      if (coop) hipLaunchKernelGGL(k_pair_step_c<G>, dim3(nblk(len / 2, 64)), dim3(256), 0, s, src, dst, len / 2);
+      else hipLaunchKernelGGL(k_pair_step<G>, dim3(nblk(len / 2, 64)), dim3(64), 0, s, src, dst, len / 2);
+    }
     MSM_HIP_CHECK(hipGetLastError());
     src = dst;
     cur ^= 1;

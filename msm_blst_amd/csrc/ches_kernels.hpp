@@ -630,7 +630,7 @@ static __global__ void __launch_bounds__(64)
 
 // blst xyzz {x, y, zzz, zz} (Montgomery R=2^384) -> internal xyzz
 template <int G>
-__global__ void k_import_xyzz(const uint64_t *__restrict__ in, Xyzz<typename FieldOf<G>::F> *__restrict__ out,
+__global__ void __launch_bounds__(256) k_import_xyzz(const uint64_t *__restrict__ in, Xyzz<typename FieldOf<G>::F> *__restrict__ out,
                               size_t n) {
   typedef typename FieldOf<G>::F F;
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -650,7 +650,7 @@ namespace msm {
 // internal xyzz -> blst xyzz {x, y, zzz, zz} (Montgomery R=2^384, canonical);
 // infinity -> all zero
 template <int G>
-__global__ void k_export_xyzz(const Xyzz<typename FieldOf<G>::F> *__restrict__ in, uint64_t *__restrict__ out,
+__global__ void __launch_bounds__(256) k_export_xyzz(const Xyzz<typename FieldOf<G>::F> *__restrict__ in, uint64_t *__restrict__ out,
                               size_t n) {
   typedef typename FieldOf<G>::F F;
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;

@@ -417,49 +417,13 @@ void Pippenger<G>::run_host(hipStream_t s, const void *pts_blst, size_t n, const
   back(s, nbits, out);
 }
 
-template <int G>
-void DenseReducer<G>::launch(hipStream_t s, const void *Abuf, int W, int S) {
-  typedef typename FieldOf<G>::F F;
-  const size_t NT = (size_t)W * S;
-  for (int k = 0; k < 2; ++k) {
-    redA[k].ensure(NT / 2 * sizeof(Xyzz<F>) + 64);
-    redY[k].ensure(NT / 2 * sizeof(Xyzz<F>) + 64);
-  }
-  fin.ensure((size_t)W * 144 * G);
-  const Xyzz<F> *A = reinterpret_cast<const Xyzz<F> *>(Abuf);
-  const Xyzz<F> *Y = nullptr;
-  int Sc = S, lvl = 0;
-  while (Sc > 1) {
-    int L = Sc >= 8 ? 8 : Sc;
-    int log2L = L == 8 ? 3 : (L == 4 ? 2 : 1);
-    Xyzz<F> *A2 = redA[lvl & 1].as<Xyzz<F>>();
-    Xyzz<F> *Y2 = redY[lvl & 1].as<Xyzz<F>>();
-    size_t threads = (size_t)W * (Sc / L);
-    hipLaunchKernelGGL(k_reduce<G>, dim3(nblk(threads, 64)), dim3(64), 0, s, A, Y, A2, Y2, Sc, L, log2L, W);
-    MSM_HIP_CHECK(hipGetLastError());
-    A = A2;
-    Y = Y2;
-    Sc /= L;
-    ++lvl;
-  }
-  if (Y == nullptr) Y = A;  // S == 1
-  hipLaunchKernelGGL(k_finalize<G>, dim3(nblk(W, 64)), dim3(64), 0, s, Y, fin.as<uint64_t>(), W);
-  MSM_HIP_CHECK(hipGetLastError());
-}
-template <int G>
-void DenseReducer<G>::read(hipStream_t s, int W, std::vector<hfp::Jac<HF>> &out) {
-  out.resize(W);
-  MSM_HIP_CHECK(hipMemcpyAsync(out.data(), fin.p, (size_t)W * sizeof(hfp::Jac<HF>), hipMemcpyDeviceToHost, s));
-  MSM_HIP_CHECK(hipStreamSynchronize(s));
-}
-template struct DenseReducer<MSM_GROUP>;
 template class Pippenger<MSM_GROUP>;
 
 // ---------------------------------------------------------------------------
 // device unit-test entry points (parity tests of the field / curve layers)
 // ---------------------------------------------------------------------------
 template <int G>
-__global__ void k_test_field(int op, const uint64_t *a, const uint64_t *b, uint64_t *out, size_t n) {
+__global__ void __launch_bounds__(64) k_test_field(int op, const uint64_t *a, const uint64_t *b, uint64_t *out, size_t n) {
   typedef typename FieldOf<G>::F F;
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -478,9 +442,26 @@ __global__ void k_test_field(int op, const uint64_t *a, const uint64_t *b, uint6
   f_to_blst(out + i * 6 * G, r);
 }
 
+// blst Jacobian (X ZZ, Y ZZZ, ZZ) of an xyzz sum, canonical; infinity -> zeros
+template <class F>
+__device__ __forceinline__ void test_export_jac(uint64_t *o, const Xyzz<F> &a) {
+  constexpr int L = (int)(sizeof(F) / sizeof(Fp)) * 18;
+  if (xyzz_is_inf(a)) {
+    for (int j = 0; j < L; ++j) o[j] = 0;
+    return;
+  }
+  F X, Y;
+  f_mul(X, a.x, a.zz);
+  f_mul(Y, a.y, a.zzz);
+  f_to_blst(o, X);
+  f_to_blst(o + L / 3, Y);
+  f_to_blst(o + 2 * L / 3, a.zz);
+}
+
 // xyzz sequences: thread i applies ops[i*len .. ] = (point index | sign<<31), then 2*acc via xyzz_add
+// (G1: one lane per sequence, the arithmetic of k_accumulate / k_segsum)
 template <int G>
-__global__ void k_test_xyzz(const uint64_t *pts_blst, const uint32_t *ops, int len, size_t nseq, uint64_t *out) {
+__global__ void __launch_bounds__(64) k_test_xyzz(const uint64_t *pts_blst, const uint32_t *ops, int len, size_t nseq, uint64_t *out) {
   typedef typename FieldOf<G>::F F;
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nseq) return;
@@ -496,23 +477,49 @@ __global__ void k_test_xyzz(const uint64_t *pts_blst, const uint32_t *ops, int l
     if (f_is_zero_exact(p.x) && f_is_zero_exact(p.y)) continue;
     xyzz_madd(acc, p, (o >> 31) != 0);
   }
-  Xyzz<F> acc2 = acc;
+  test_export_jac(out + i * 2 * 18 * G, acc);
   Xyzz<F> a1 = acc;
-  xyzz_add(acc2, a1);
-  Xyzz<F> res[2] = {acc, acc2};
-  for (int k = 0; k < 2; ++k) {
-    uint64_t *o = out + (i * 2 + k) * 18 * G;
-    if (xyzz_is_inf(res[k])) {
-      for (int j = 0; j < 18 * G; ++j) o[j] = 0;
-      continue;
-    }
-    F X, Y;
-    f_mul(X, res[k].x, res[k].zz);
-    f_mul(Y, res[k].y, res[k].zzz);
-    f_to_blst(o, X);
-    f_to_blst(o + 6 * G, Y);
-    f_to_blst(o + 12 * G, res[k].zz);
+  xyzz_add(acc, a1);
+  test_export_jac(out + (i * 2 + 1) * 18 * G, acc);
+}
+
+// the same for G2 on lane pairs (fp2l.hpp), the arithmetic every G2 product
+// kernel runs (k_accumulate2p, k_segsum2p, the lane-pair tails): lanes 2i,
+// 2i + 1 hold component 0 / 1 of sequence i
+__device__ __forceinline__ void test_export_jac2l(uint64_t *o, const Xyzz<Fp2L> &a, int comp) {
+  if (xyzz_is_inf(a)) {  // uniform per pair
+    for (int j = 0; j < 6; ++j) o[6 * comp + j] = o[12 + 6 * comp + j] = o[24 + 6 * comp + j] = 0;
+    return;
   }
+  Fp2L X, Y;
+  f_mul(X, a.x, a.zz);
+  f_mul(Y, a.y, a.zzz);
+  fp_to_blst(o + 6 * comp, X.c);
+  fp_to_blst(o + 12 + 6 * comp, Y.c);
+  fp_to_blst(o + 24 + 6 * comp, a.zz.c);
+}
+static __global__ void __launch_bounds__(64)
+    k_test_xyzz2p(const uint64_t *pts_blst, const uint32_t *ops, int len, size_t nseq, uint64_t *out) {
+  const size_t tt = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tt >= 2 * nseq) return;  // whole pairs only
+  const int comp = (int)(tt & 1);
+  const size_t i = tt >> 1;
+  Xyzz<Fp2L> acc;
+  xyzz_set_inf(acc);
+  for (int k = 0; k < len; ++k) {
+    uint32_t o = ops[i * len + k];
+    if (o == 0xffffffffu) continue;
+    Aff<Fp2L> p;
+    const uint64_t *src = pts_blst + (size_t)(o & 0x7fffffffu) * 24;
+    fp_from_blst(p.x.c, src + 6 * comp);
+    fp_from_blst(p.y.c, src + 12 + 6 * comp);
+    if (f_is_zero_exact(p.x) && f_is_zero_exact(p.y)) continue;
+    xyzz_madd(acc, p, (o >> 31) != 0);
+  }
+  test_export_jac2l(out + i * 2 * 36, acc, comp);
+  Xyzz<Fp2L> a1 = acc;
+  xyzz_add(acc, a1);
+  test_export_jac2l(out + (i * 2 + 1) * 36, acc, comp);
 }
 
 template <int G>
@@ -537,8 +544,12 @@ void test_xyzz(const uint64_t *pts, size_t npts, const uint32_t *ops, int len, s
   dout.ensure(nseq * 2 * 144 * G);
   MSM_HIP_CHECK(hipMemcpy(dp.p, pts, npts * 96 * G, hipMemcpyHostToDevice));
   MSM_HIP_CHECK(hipMemcpy(dops.p, ops, nseq * len * 4, hipMemcpyHostToDevice));
-  hipLaunchKernelGGL(k_test_xyzz<G>, dim3(nblk(nseq, 64)), dim3(64), 0, 0, dp.as<uint64_t>(), dops.as<uint32_t>(), len,
-                     nseq, dout.as<uint64_t>());
+  if constexpr (G == 2)
+    hipLaunchKernelGGL(k_test_xyzz2p, dim3(nblk(2 * nseq, 64)), dim3(64), 0, 0, dp.as<uint64_t>(), dops.as<uint32_t>(),
+                       len, nseq, dout.as<uint64_t>());
+  else
+    hipLaunchKernelGGL(k_test_xyzz<G>, dim3(nblk(nseq, 64)), dim3(64), 0, 0, dp.as<uint64_t>(), dops.as<uint32_t>(),
+                       len, nseq, dout.as<uint64_t>());
   MSM_HIP_CHECK(hipGetLastError());
   MSM_HIP_CHECK(hipMemcpy(out, dout.p, nseq * 2 * 144 * G, hipMemcpyDeviceToHost));
 }

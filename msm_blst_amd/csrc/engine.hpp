@@ -114,18 +114,6 @@ struct BucketSort {
   }
 };
 
-// Dense windowed bucket reduction: for each of W windows of S buckets
-// (A[w*S + b-1] holds bucket value b), T_w = sum_b b * A_b, read back to host
-// as blst Jacobians.  Shared by the Pippenger and CHES pipelines.
-template <int G>
-struct DenseReducer {
-  typedef typename HostField<G>::F HF;
-  DevBuf redA[2], redY[2], fin;
-  // A: device array of W*S internal xyzz points; enqueues the reduction levels
-  void launch(hipStream_t s, const void *A, int W, int S);
-  // enqueue the read-back of the W window totals and wait for it
-  void read(hipStream_t s, int W, std::vector<hfp::Jac<HF>> &out);
-};
 // sum_w 2^(c w) T_w, Horner from the top window (ref multi_scalar.c:565-575)
 template <class HF>
 hfp::Jac<HF> horner(const std::vector<hfp::Jac<HF>> &T, int c) {

@@ -9,7 +9,8 @@
 //                 bucket schedule = ids sorted by count, descending, so a
 //                 wavefront's 64 buckets are equally long
 //   k_accumulate  one lane per bucket: xyzz += +-P over its sorted points
-//   k_reduce      segmented running sums, log_L(NB) levels (sum_b b*B_b)
+//   reduction     WeightedReducer (ches.hip): segment sums by weight bits,
+//                 dense suffix-scan stage (sum_b b*B_b)
 //   k_finalize    window totals -> blst Jacobian (R=2^384 Montgomery)
 // CHES pipeline: see ches.hpp.
 #pragma once
@@ -304,55 +305,12 @@ __global__ void __launch_bounds__(256, MSM_ACC_WAVES)
   if (t < nbuckets) accumulate_bucket<G>(S, pts, buckets, t);
 }
 
-// One level of the bucket reduction.  Invariant per window:
-//   Total = sum_s Y_s + sum_s s * A_s,  s in [0, S)
-// Thread (w, s2) folds s = s2*L + j, j in [0, L):
-//   a = sum_j A_j,  r = sum_j j A_j (running sums),  Y' = sum_j Y_j + r,  A' = L * a
-// First level: A_s = bucket s+1 and Y_s = A_s (sum_b b B_b = sum_s (s+1) A_s).
-template <int G>
-__global__ void __launch_bounds__(256) k_reduce(const Xyzz<typename FieldOf<G>::F> *__restrict__ A,
-                                                const Xyzz<typename FieldOf<G>::F> *__restrict__ Y,
-                                                Xyzz<typename FieldOf<G>::F> *__restrict__ A2,
-                                                Xyzz<typename FieldOf<G>::F> *__restrict__ Y2, int S, int L,
-                                                int log2L, int W) {
-  typedef typename FieldOf<G>::F F;
-  int S2 = S / L;
-  size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (size_t)W * S2) return;
-  size_t w = t / S2, s2 = t - w * S2;
-  const Xyzz<F> *Aw = A + w * S + s2 * L;
-  Xyzz<F> acc, r, y;
-  xyzz_set_inf(acc);
-  xyzz_set_inf(r);
-  for (int j = L - 1; j >= 1; --j) {
-    Xyzz<F> a = ld16(&Aw[j]);
-    xyzz_add(acc, a);
-    xyzz_add(r, acc);
-  }
-  Xyzz<F> a0 = ld16(&Aw[0]);
-  xyzz_add(acc, a0);
-  if (Y == nullptr) {
-    y = acc;
-  } else {
-    const Xyzz<F> *Yw = Y + w * S + s2 * L;
-    y = ld16(&Yw[0]);
-    for (int j = 1; j < L; ++j) {
-      Xyzz<F> v = ld16(&Yw[j]);
-      xyzz_add(y, v);
-    }
-  }
-  xyzz_add(y, r);
-  for (int k = 0; k < log2L; ++k) {
-    Xyzz<F> tmp = acc;
-    xyzz_dbl(acc, tmp);
-  }
-  st16(&A2[w * S2 + s2], acc);
-  st16(&Y2[w * S2 + s2], y);
-}
-
 // xyzz -> blst Jacobian (X*ZZ, Y*ZZZ, ZZ)  (ref ec_ops.h:771-777), canonical blst Montgomery
+// (one lane per window, 64-thread blocks: the bound lets G2 keep every operand
+// in registers -- the default 1024-thread bound capped it at 128 VGPRs and
+// spilled 236 B, tests/test_kernel_resources.py)
 template <int G>
-__global__ void k_finalize(const Xyzz<typename FieldOf<G>::F> *__restrict__ T, uint64_t *__restrict__ out, int W) {
+__global__ void __launch_bounds__(64) k_finalize(const Xyzz<typename FieldOf<G>::F> *__restrict__ T, uint64_t *__restrict__ out, int W) {
   typedef typename FieldOf<G>::F F;
   int w = blockIdx.x * blockDim.x + threadIdx.x;
   if (w >= W) return;

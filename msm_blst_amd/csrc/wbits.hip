@@ -5,7 +5,7 @@
 //
 // Table (reference layout, ref multi_scalar.c:82-91): row i holds the nwin =
 // 2^(wbits-1) canonical affine multiples (k+1) P_i, k < nwin.  Built on the GPU
-// by k_wbits_table: one lane per point, nwin xyzz multiples by repeated mixed
+// by k_wbits_table (G2: k_wbits_table2p, a lane pair per point): one lane per point, nwin xyzz multiples by repeated mixed
 // additions, then one Montgomery batch inversion per lane (the reference does
 // the same per stride of rows, ref :94-120).
 //
@@ -22,6 +22,7 @@
 
 #include "ches_kernels.hpp"
 #include "engine.hpp"
+#include "pair_kernels.hpp"
 
 #ifndef MSM_GROUP
 #error "define MSM_GROUP (1 or 2)"
@@ -31,7 +32,7 @@ namespace msm {
 
 // one lane per point i in [i0, i0 + cnt): T[i nwin + k] = (k+1) P_i
 template <int G>
-static __global__ void __launch_bounds__(256)
+static __global__ void __launch_bounds__(64)
     k_wbits_table(const Aff<typename FieldOf<G>::F> *__restrict__ P, size_t i0, size_t cnt, int nwin,
                   Xyzz<typename FieldOf<G>::F> *__restrict__ scratch, typename FieldOf<G>::F *__restrict__ pref,
                   AffP<typename FieldOf<G>::F> *__restrict__ T) {
@@ -132,6 +133,102 @@ static __global__ void __launch_bounds__(256)
   st16(&parts[t], acc);
 }
 
+// G2 on lane pairs (fp2l.hpp; as k_ches_table2p / k_accumulate2p): lanes 2t,
+// 2t + 1 handle point t, one Fp2 component each.  The one-lane G2 kernels
+// needed 256 VGPRs + 256 AGPRs and spilled (k_wbits_table<2>: 140 B of
+// scratch; k_wbits_sums<2>: 9 VGPRs to AGPRs); a lane holds half the state here
+// (tests/test_kernel_resources.py keeps every product kernel spill-free).
+static __global__ void __launch_bounds__(128)
+    k_wbits_table2p(const Aff<Fp2> *__restrict__ P, size_t i0, size_t cnt, int nwin, Xyzz<Fp2> *__restrict__ scratch,
+                    Fp2 *__restrict__ pref, AffP<Fp2> *__restrict__ T) {
+  const size_t tt = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tt >= 2 * cnt) return;  // whole pairs only
+  const int comp = (int)(tt & 1);
+  const size_t t = tt >> 1, i = i0 + t;
+  Aff<Fp2L> p;
+  ld_point2l(p, &P[i], comp);
+  AffP<Fp2> *out = T + (size_t)nwin * i;
+  if (f_is_zero_exact(p.x) && f_is_zero_exact(p.y)) {  // infinity: every multiple is infinity (uniform per pair)
+    Fp z;
+    fp_zero(z);
+    for (int k = 0; k < nwin; ++k) {
+      Aff<Fp2> *o = reinterpret_cast<Aff<Fp2> *>(out + k);
+      st_comp(&o->x, z, comp);
+      st_comp(&o->y, z, comp);
+    }
+    return;
+  }
+  Xyzz<Fp2L> Q;
+  xyzz_from_aff(Q, p, false);
+  for (int k = 0; k < nwin; ++k) {
+    st_xyzz2l(&scratch[(size_t)k * cnt + t], Q, comp);
+    if (k + 1 < nwin) xyzz_madd(Q, p, false);  // (k+2) P; the k = 0 step takes the doubling branch
+  }
+  Fp2L c;  // Montgomery batch inversion of u_k = ZZ_k ZZZ_k, as k_wbits_table
+  f_one(c);
+  for (int k = 0; k < nwin; ++k) {
+    Xyzz<Fp2L> a;
+    ld_xyzz2l(a, &scratch[(size_t)k * cnt + t], comp);
+    Fp2L u;
+    f_mul(u, a.zz, a.zzz);
+    f_mul(c, c, u);
+    st_comp(&pref[(size_t)k * cnt + t], c.c, comp);
+  }
+  Fp2L inv;
+  f_inv(inv, c);
+  for (int k = nwin - 1; k >= 0; --k) {
+    Xyzz<Fp2L> a;
+    ld_xyzz2l(a, &scratch[(size_t)k * cnt + t], comp);
+    Fp2L ik;
+    if (k > 0) {
+      Fp2L pk;
+      ld_comp(pk.c, &pref[(size_t)(k - 1) * cnt + t], comp);
+      f_mul(ik, inv, pk);
+      Fp2L u;
+      f_mul(u, a.zz, a.zzz);
+      f_mul(inv, inv, u);
+    } else {
+      ik = inv;
+    }
+    Fp2L izz, izzz, x, y;
+    f_mul(izz, ik, a.zzz);
+    f_mul(izzz, ik, a.zz);
+    f_mul(x, a.x, izz);
+    f_mul(y, a.y, izzz);
+    f_csub(x);
+    f_csub(y);
+    Aff<Fp2> *o = reinterpret_cast<Aff<Fp2> *>(out + k);
+    st_comp(&o->x, x.c, comp);
+    st_comp(&o->y, y.c, comp);
+  }
+}
+
+// k_wbits_sums for G2: lane pair (w, c), both lanes read the same digits
+static __global__ void __launch_bounds__(256)
+    k_wbits_sums2p(const AffP<Fp2> *__restrict__ T, int wbits, const uint8_t *__restrict__ sc, size_t stride, int nbits,
+                   size_t n, int nw, size_t nch, size_t C, Xyzz<Fp2> *__restrict__ parts) {
+  const size_t tt = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tt >= 2 * (size_t)nw * nch) return;
+  const int comp = (int)(tt & 1);
+  const size_t t = tt >> 1;
+  const int w = (int)(t / nch);
+  const size_t c = t % nch, nwin = (size_t)1 << (wbits - 1);
+  Xyzz<Fp2L> acc;
+  xyzz_set_inf(acc);
+  const size_t e = min(n, (c + 1) * C);
+  for (size_t i = c * C; i < e; ++i) {
+    const uint32_t wval = wbits_field(sc + i * stride, nbits, w * wbits - 1, wbits + 1);
+    const int d = (int)((wval + 1) >> 1) - (int)((wval >> wbits) << wbits);  // booth_encode, ec_mult.h:46-55
+    if (d == 0) continue;
+    const uint32_t m = (uint32_t)(d < 0 ? -d : d);
+    Aff<Fp2L> p;
+    ld_point2l(p, &T[i * nwin + m - 1], comp);
+    if (f_is_zero_exact(p.x) && f_is_zero_exact(p.y)) continue;  // infinity row (uniform per pair)
+    xyzz_madd(acc, p, d < 0);
+  }
+  st_xyzz2l(&parts[t], acc, comp);
+}
+
 // per window: dst[w nout + j] = src[w nin + 2j] + src[w nin + 2j + 1]
 template <int G>
 static __global__ void __launch_bounds__(64)
@@ -184,8 +281,12 @@ void Wbits<G>::precompute(const void *pts, size_t n, bool on_device, hipStream_t
   pref.ensure(nwin * chunk * sizeof(F));
   for (size_t i0 = 0; i0 < n; i0 += chunk) {
     const size_t cnt = std::min(chunk, n - i0);
-    hipLaunchKernelGGL(k_wbits_table<G>, dim3(nblk(cnt, 64)), dim3(64), 0, s, base.as<Aff<F>>(), i0, cnt, (int)nwin,
-                       scratch.as<Xyzz<F>>(), pref.as<F>(), table_.as<AffP<F>>());
+    if constexpr (G == 2)
+      hipLaunchKernelGGL(k_wbits_table2p, dim3(nblk(2 * cnt, 128)), dim3(128), 0, s, base.as<Aff<F>>(), i0, cnt,
+                         (int)nwin, scratch.as<Xyzz<F>>(), pref.as<F>(), table_.as<AffP<F>>());
+    else
+      hipLaunchKernelGGL(k_wbits_table<G>, dim3(nblk(cnt, 64)), dim3(64), 0, s, base.as<Aff<F>>(), i0, cnt,
+                         (int)nwin, scratch.as<Xyzz<F>>(), pref.as<F>(), table_.as<AffP<F>>());
     MSM_HIP_CHECK(hipGetLastError());
   }
   MSM_HIP_CHECK(hipStreamSynchronize(s));
@@ -249,8 +350,12 @@ void Wbits<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, int n
   parts_[0].ensure((size_t)nw * nch * sizeof(Xyzz<F>));
   parts_[1].ensure((size_t)nw * ((nch + 1) / 2 + 1) * sizeof(Xyzz<F>));
   fin_.ensure((size_t)nw * 144 * G);
-  hipLaunchKernelGGL(k_wbits_sums<G>, dim3(nblk((size_t)nw * nch, 256)), dim3(256), 0, s, table_.as<AffP<F>>(),
-                     wbits_, d_scalars, stride, nbits, n_, nw, nch, C, parts_[0].as<Xyzz<F>>());
+  if constexpr (G == 2)
+    hipLaunchKernelGGL(k_wbits_sums2p, dim3(nblk(2 * (size_t)nw * nch, 256)), dim3(256), 0, s, table_.as<AffP<F>>(),
+                       wbits_, d_scalars, stride, nbits, n_, nw, nch, C, parts_[0].as<Xyzz<F>>());
+  else
+    hipLaunchKernelGGL(k_wbits_sums<G>, dim3(nblk((size_t)nw * nch, 256)), dim3(256), 0, s, table_.as<AffP<F>>(),
+                       wbits_, d_scalars, stride, nbits, n_, nw, nch, C, parts_[0].as<Xyzz<F>>());
   MSM_HIP_CHECK(hipGetLastError());
   int cur = 0;
   while (nch > 1) {

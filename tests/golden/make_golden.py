@@ -9,6 +9,8 @@ Runs only in the build container (where /root/reference exists):
 Every fixture is data (inputs and expected outputs); no reference source
 text is stored.  Test infrastructure only.
 
+`python make_golden.py large` only appends the large G1 seed-1 keys (LARGE_G1).
+
 Fixtures written:
   msm_g1.json / msm_g2.json  compressed MSM results of blst_p{1,2}s_mult_pippenger
                              (seeded scalars, P_i = 2^(i+1) G), incl. edge cases
@@ -37,6 +39,31 @@ def run(args):
     return subprocess.run(args, check=True, capture_output=True, text=True).stdout
 
 
+# seed-1 keys at the strong-scaling shard sizes (2^20 / N points per rank,
+# N = 8, 4, 2) and the weak-scaling totals (2^20 per rank: 2^22 at N = 4, 2^23
+# at N = 8), so every multi-rank bench leg has a parity pin
+LARGE_G1 = [(1 << e, 1, 255, "rand") for e in (17, 18, 19, 22, 23)]
+
+
+def msm_case(group, n, seed, nbits, cas):
+    t = time.time()
+    res = run([os.path.join(BIN, "ref_golden"), "msm", str(group), str(n), str(seed), str(nbits), cas]).strip()
+    print(f"G{group} n={n} seed={seed} nbits={nbits} {cas}: {res[:16]}.. ({time.time()-t:.1f}s)", file=sys.stderr)
+    return {"group": group, "n": n, "seed": seed, "nbits": nbits, "case": cas, "compressed": res}
+
+
+def add_large():
+    """Append LARGE_G1 to msm_g1.json (the other cases unchanged)."""
+    subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "ref", f"REF={REF}"], check=True)
+    fn = os.path.join(HERE, "msm_g1.json")
+    d = json.load(open(fn))
+    have = {(c["n"], c["seed"], c["nbits"], c["case"]) for c in d["cases"]}
+    for (n, seed, nbits, cas) in LARGE_G1:
+        if (n, seed, nbits, cas) not in have:
+            d["cases"].append(msm_case(1, n, seed, nbits, cas))
+    json.dump(d, open(fn, "w"), indent=1)
+
+
 def msm_cases():
     g1, g2 = [], []
     for n in (2, 3, 4, 5, 7, 8, 16, 31, 32, 64, 100, 128, 256, 512, 1000, 1024):
@@ -46,6 +73,7 @@ def msm_cases():
         for seed in (1, 2):
             g1.append((n, seed, 255, "rand"))
     g1 += [(1 << 20, 1, 255, "rand"), (1 << 21, 1, 255, "rand")]
+    g1 += LARGE_G1
     for cas in ("zero", "ones", "rminus1", "equal", "negpairs", "ptr"):
         g1.append((64, 1, 255, cas))
     for nbits in (64, 128, 256):
@@ -68,10 +96,7 @@ def main():
     for group, cases, fname in ((1, g1, "msm_g1.json"), (2, g2, "msm_g2.json")):
         out = []
         for (n, seed, nbits, cas) in cases:
-            t = time.time()
-            res = run([os.path.join(BIN, "ref_golden"), "msm", str(group), str(n), str(seed), str(nbits), cas]).strip()
-            out.append({"group": group, "n": n, "seed": seed, "nbits": nbits, "case": cas, "compressed": res})
-            print(f"G{group} n={n} seed={seed} nbits={nbits} {cas}: {res[:16]}.. ({time.time()-t:.1f}s)", file=sys.stderr)
+            out.append(msm_case(group, n, seed, nbits, cas))
         json.dump({"source": "reference libblst blst_p%ds_mult_pippenger via oracle/ref_golden.c" % group,
                    "points": "P_i = 2^(i+1) G (main_p1.cpp:52-66)",
                    "scalars": "SplitMix64(seed), 4 LE words, word3 >>= 1, reject >= r; packed flat with stride (nbits+7)/8",
@@ -126,7 +151,9 @@ def drivers():
 
 
 if __name__ == "__main__":
-    if sys.argv[1:] == ["drivers"]:
+    if sys.argv[1:] == ["large"]:
+        add_large()
+    elif sys.argv[1:] == ["drivers"]:
         subprocess.run(["make", "-C", os.path.join(REPO, "oracle"), "ref", f"REF={REF}"], check=True)
         drivers()
     else:
