@@ -56,6 +56,18 @@ FPMUL_PER_MADD = 10            # 8M + 2S (ec_ops.h:727-748)
 MAD_RATE = 30.36e12            # measured chip v_mad_u64_u32 issue rate (lane-ops/s): profiles/r02_instr_rate.txt
 CPU_THREADS = 16               # the GPU box's CPU share per GPU (16 threads)
 DEFAULT_BETA = {}              # log_n -> ches_config_files variant used by default; _beta at 2^20 measured slower
+# CHES configuration per point count (n_exp, beta of a ches_config_files header; its q, h and a_h are valid
+# for any point count): the strong-scaling shards of `--gpus N` (2^20 / N points per rank) take the
+# configuration MEASURED fastest for that shard size on MI355X (tools/shard_study.py,
+# profiles/r05_shard_study.txt), not necessarily the reference's config_file_n_exp_<log2 shard>.h
+SHARD_CONFIG = {}
+
+
+def ches_config(log_n, beta=None):
+    """(n_exp, beta) of the CHES configuration for 2^log_n points per GPU."""
+    if beta is not None:
+        return log_n, beta
+    return SHARD_CONFIG.get(log_n, (log_n, DEFAULT_BETA.get(log_n, 0)))
 
 
 def isa_mads_per_madd(G=1, path=os.path.join(REPO, "profiles", "r04_isa_counts.txt")):
@@ -161,6 +173,8 @@ def main():
                          "profiles/r04_setup_batch_ab.txt)")
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the other BASELINE configs' legs (configs[0], [1], [4], the blst drop-in at 2^20)")
+    ap.add_argument("--no-shards", action="store_true",
+                    help="N = 1: skip the one-GPU projection of the N = 2/4/8 strong-scaling shards")
     ap.add_argument("--cpu-sample-log-n", type=int, default=20)
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
@@ -222,23 +236,24 @@ def main():
             return parts
         return [mdist.fold(ps, add) for ps in mdist.gather_partials_batch(parts, G, xdev)]
 
+    cfg_n, beta = ches_config(args.log_n, args.beta)  # the config file this point count uses (SHARD_CONFIG)
+
     def has_config(b):
         try:
-            m.ches.params(args.log_n, b)
+            m.ches.params(cfg_n, b)
             return True
         except Exception:
             return False
 
-    beta = args.beta if args.beta is not None else DEFAULT_BETA.get(args.log_n, 0)
     if not has_config(beta):
-        log(f"no reference configuration n_exp={args.log_n} beta={beta}; using beta=0")
-        beta = 0
+        log(f"no reference configuration n_exp={cfg_n} beta={beta}; using n_exp={args.log_n} beta=0")
+        cfg_n, beta = args.log_n, 0
 
     def make(method, b=None):
         t = time.time()
         b = beta if b is None else b
         if method == "ches":
-            ctx = m.CHESContext(G, local, n_exp=args.log_n, beta=b)
+            ctx = m.CHESContext(G, local, n_exp=cfg_n, beta=b)
             ctx.build_table(pts, n, stream=sp)
         elif method == "bgmw":
             ctx = m.BGMWContext(G, local, n_exp=args.log_n, beta=b)
@@ -301,7 +316,7 @@ def main():
                     "kernel_ms": round(octx.phase_times()["accumulate"], 4),
                     "equals_h2d_batch": keys(oparts) == keys(res),
                     "note": f"the reference's other n=2^{args.log_n} configuration "
-                            f"(config_file_n_exp_{args.log_n}{'_beta' if beta == 0 else ''}.h: q=2^{op['q_exp']}, "
+                            f"(config_file_n_exp_{cfg_n}{'_beta' if beta == 0 else ''}.h: q=2^{op['q_exp']}, "
                             f"h={op['h']}, |B|={op['b_size']}), same K resident sets"}
                 octx.close()
             sres, sel = sync_steps(mult, K, True)
@@ -353,6 +368,8 @@ def main():
                              "parity_vs_reference": (m.compress(G, ores[0]).hex() == want[0]) if want else None}
             octx.close()
 
+    if world == 1 and not args.no_compare and not args.no_shards and G == 1 and args.log_n == 20 and batched:
+        others.update(shard_legs(m, mdist, torch, dev, local, sp, host, K, W, n * K / elapsed))
     if world == 1 and not args.no_compare and not args.no_configs and G == 1 and args.log_n == 20:
         others.update(config_legs(m, torch, dev, local, sp, pts, host, K, W))
     # configs[3]: G1 n = 2^21 sharded over the ranks (RCCL path) or over the
@@ -383,7 +400,7 @@ def main():
                     f"|B|={ctx.params['b_size']}), table T=m*q^j*P_i resident in HBM, K distinct scalar sets "
                     f"H2D from pinned host memory inside the timed region")
         cfg_extra = {"method": "ches_q_over_5", "beta": beta,
-                     "config_file": f"ches_config_files/config_file_n_exp_{args.log_n}{'_beta' if beta else ''}.h",
+                     "config_file": f"ches_config_files/config_file_n_exp_{cfg_n}{'_beta' if beta else ''}.h",
                      "q_exp": ctx.params["q_exp"], "h": h,
                      "bucket_set": ctx.params["b_size"], "buckets_incl_top_digit_copies": ctx.bucket_count()}
     elif args.method == "bgmw":
@@ -700,6 +717,8 @@ def tile_d_ches_legs(m, pts, host):
     L = m.lib()
     L.blst_p1_construct_nh_scalars_nh_points.argtypes = [vp, vp, vp, sz, vp, vp]
     L.blst_p1_tile_pippenger_d_CHES.argtypes = [vp, vp, sz, vp, vp, vp, vp, vp, sz, i32]
+    L.msm_register_host_table.argtypes = [i32, vp, sz]
+    L.msm_unregister_host_table.argtypes = [vp]
     legs = {}
     hv = host.numpy()
     for lg in (16, 20):
@@ -745,8 +764,87 @@ def tile_d_ches_legs(m, pts, host):
             "note": f"main_p1.cpp:249-291 sequence (q=2^{p['q_exp']}, h={h}): digits + construct_nh (host, not timed), "
                     f"then the timed blst_p1_tile_pippenger_d_CHES over {ne} row pointers into the host table; the "
                     f"context's synchronous MSM on the same set for comparison (ctx_sync_ms, scalars H2D)"}
+        # the same calls after registering the host table once (msm_register_host_table): row indices
+        # instead of gathered rows
+        t = time.perf_counter()
+        rc = L.msm_register_host_table(1, T, 3 * n * h)
+        reg_s = time.perf_counter() - t
+        if rc == 0:
+            L.blst_p1_tile_pippenger_d_CHES(ret, ptrs, ne, nh, signs, buckets, B, v2i, len(B), p["d_max"])
+            t = time.perf_counter()
+            for _ in range(reps):
+                L.blst_p1_tile_pippenger_d_CHES(ret, ptrs, ne, nh, signs, buckets, B, v2i, len(B), p["d_max"])
+            el = (time.perf_counter() - t) / reps
+            L.msm_unregister_host_table(T)
+            legs[f"blst_p1_tile_pippenger_d_CHES_2^{lg}_registered"] = {
+                "value": round(n / el, 1), "unit": "pairs/s", "ms_per_step": round(el * 1e3, 4),
+                "ctx_sync_ms": round(sync_ms, 4), "ratio_vs_ctx_sync": round(el * 1e3 / sync_ms, 2),
+                "register_s": round(reg_s, 3),
+                "parity_vs_reference": m.compress(1, bytes(ret)).hex() == _golden(m, 1, n),
+                "note": f"the same tile calls after msm_register_host_table(1, T, {3 * n * h}) once (not timed): "
+                        f"the {ne} pointers travel as 4-B row indices into the device copy of T, no row gather; "
+                        f"the buckets are still exported into the caller's array as the reference leaves them"}
         del T, ptrs, nh, signs, buckets
     return legs
+
+
+def shard_legs(m, mdist, torch, dev, local, sp, host, K, W, headline_value):
+    """The metric's N-GPU strong-scaling shards, measured on ONE GPU (a
+    projection, not a scaling number): the 2^20 problem of the headline split
+    into N = 2, 4, 8 contiguous shards exactly as `bench.py --gpus N` splits it
+    (rank r: points [r 2^20/N, (r+1) 2^20/N), the CHES configuration
+    ches_config(20 - log2 N), the r-th slice of each of the K pinned host sets).
+    Every shard runs the same pipelined H2D batch of K sets the rank would run,
+    one shard after another on device 0; per_shard_ms = the slowest shard's ms
+    per MSM, projected_value = 2^20 K / (K per_shard_ms) -- the N-GPU rate if
+    the ranks ran at this speed side by side with a free exchange -- and
+    efficiency = projected_value / (N x the headline value).  Parity: set 0's
+    shard partials folded (exact host add) against the 2^20 golden; each shard's
+    batch against its synchronous MSM on sets 0 and K-1."""
+    n20, SS = 1 << 20, 32 << 20
+    add = mdist.engine_add(1)
+    want = _golden(m, 1, n20)
+    hptr = host.data_ptr()
+    out = {}
+    for N in (2, 4, 8):
+        n = n20 // N
+        lg = n.bit_length() - 1
+        n_exp, cbeta = ches_config(lg)
+        times, parts0, eqs, setup, params = [], [], [], 0.0, None
+        for r in range(N):
+            t = time.time()
+            ctx = m.CHESContext(1, local, n_exp=n_exp, beta=cbeta)
+            ctx.build_table(m.fixed_points(1, n, r * n), n, stream=sp)
+            torch.cuda.synchronize(dev)
+            setup += time.time() - t
+            params = ctx.params
+            base = hptr + r * n * 32
+            ctx.mult_batch(base, min(max(W, 1), K), 32, set_stride=SS, on_device=False, stream=sp)
+            torch.cuda.synchronize(dev)
+            t = time.perf_counter()
+            res = ctx.mult_batch(base, K, 32, set_stride=SS, on_device=False, stream=sp)
+            torch.cuda.synchronize(dev)
+            times.append(time.perf_counter() - t)
+            parts0.append(res[0])
+            sync = [ctx.mult(base + k * SS, 32, on_device=False, stream=sp) for k in (0, K - 1)]
+            eqs.append([m.compress(1, x) for x in sync] == [m.compress(1, res[0]), m.compress(1, res[K - 1])])
+            lanes = ctx.batch_lanes()
+            ctx.close()
+        worst = max(times)
+        proj = n20 * K / worst
+        folded = mdist.fold(parts0, add)
+        out[f"shards_2^20_over_{N}_one_gpu"] = {
+            "value": None, "projected_value": round(proj, 1), "unit": "pairs/s",
+            "per_shard_ms": round(worst / K * 1e3, 4), "shard_ms_all": [round(x / K * 1e3, 4) for x in times],
+            "efficiency": round(proj / (N * headline_value), 4),
+            "parity_vs_reference": m.compress(1, folded).hex() == want if want else None,
+            "batch_equals_sync_all_shards": all(eqs), "points_per_shard": n, "lanes": lanes,
+            "config": f"config_file_n_exp_{n_exp}{'_beta' if cbeta else ''}.h: q=2^{params['q_exp']}, h={params['h']}, "
+                      f"|B|={params['b_size']}", "setup_s": round(setup, 2),
+            "note": f"ONE-GPU PROJECTION, not a scaling number: the {N} shards of `bench.py --gpus {N}` run one after "
+                    f"another on device 0, each its own {K}-set H2D batch; projected_value = 2^20 x {K} / slowest "
+                    f"shard's batch time; efficiency = projected_value / ({N} x headline)"}
+    return out
 
 
 def _cfg3_sets(m, K, lo, hi):
@@ -803,9 +901,9 @@ def cfg3_ranks(m, mdist, torch, dev, local, sp, world, rank, K, W, xdev, add):
     N = 1 << 21
     lo, hi = mdist.shard_range(N, world, rank)
     n = hi - lo
-    n_exp = n.bit_length() - 1
+    n_exp, cbeta = ches_config(n.bit_length() - 1)
     t = time.time()
-    ctx = m.CHESContext(1, local, n_exp=n_exp)
+    ctx = m.CHESContext(1, local, n_exp=n_exp, beta=cbeta)
     ctx.build_table(m.fixed_points(1, n, lo), n, stream=sp)
     host = _cfg3_sets(m, K, lo, hi)
     torch.cuda.synchronize(dev)
@@ -821,7 +919,7 @@ def cfg3_ranks(m, mdist, torch, dev, local, sp, world, rank, K, W, xdev, add):
         "value": round(N * K / b.elapsed, 1), "unit": "pairs/s", "ms_per_step": round(b.elapsed / K * 1e3, 4),
         "parity_vs_reference": ok, "setup_s": round(setup, 2), "points_per_rank": n,
         "note": f"configs[3]: G1 n=2^21 over {world} ranks ({n} points each, config_file_n_exp_{n_exp}.h), "
-                f"{K} distinct scalar sets H2D from pinned memory, one RCCL all_gather of the batch's partials"}}
+                f"{K} distinct scalar sets H2D from pinned memory, one all_gather of the batch's partials"}}
 
 
 def cfg3_multi_context(m, torch, D, one_device, K, W):

@@ -204,6 +204,20 @@ int msm_device_count(void);
 void msm_release_engine_cache(void);
 void msm_engine_cache_stats(size_t out[3]);
 size_t msm_set_engine_cache_limit(size_t bytes);
+/* Registered host tables (extension for the pointer-array tiles above).  The
+ * reference driver hands the SAME host table to every CHES tile call, as one
+ * pointer per entry into PRECOMPUTATION_POINTS_LIST_3nh (ref main_p1.cpp:233-236,
+ * :279-282; 3 n h rows, built once by init_pippenger_CHES_q_over_5 :128-178).
+ * Registering those rows once uploads them to the current device; afterwards a
+ * tile call (blst_p{1,2}_tile_pippenger_d_CHES, _noindexhash, _BGMW95) whose
+ * pointers all lie on row boundaries inside one registered table sends 4-B row
+ * indices instead of gathering and uploading every 96/192-B row (1.2 GB per
+ * G1 2^20 call).  Any pointer outside the table falls back to the gather.  The
+ * caller must not modify or free the rows while they are registered (as with
+ * hipHostRegister).  group 1 (G1, blst_p1_affine rows) or 2 (G2); registering
+ * an already registered base replaces it.  Returns MSM_OK or an error code. */
+int msm_register_host_table(int group, const void *rows_affine, size_t nrows);
+int msm_unregister_host_table(const void *rows_affine);
 /* group 1 (G1) or 2 (G2); points in blst affine layout, host or device memory */
 int msm_ctx_create(msm_ctx **ctx, int group, int device, int window_bits);
 int msm_ctx_set_points(msm_ctx *ctx, const void *points_affine, size_t npoints, int points_on_device,

@@ -68,6 +68,8 @@ def lib():
     L.msm_ches_ctx_phase_times.argtypes = [vp, vp]
     L.msm_ches_ctx_bucket_count.argtypes = [vp]
     L.msm_ches_ctx_bucket_count.restype = sz
+    L.msm_register_host_table.argtypes = [i32, vp, sz]
+    L.msm_unregister_host_table.argtypes = [vp]
     L.msm_ches_ctx_batch_lanes.argtypes = [vp]
     L.msm_ches_ctx_destroy.argtypes = [vp]
     L.msm_ches_ctx_destroy.restype = None

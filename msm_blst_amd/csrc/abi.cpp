@@ -20,6 +20,7 @@
 #include "engine.hpp"
 #include "multi.hpp"
 #include "pool.hpp"
+#include "table_registry.hpp"
 
 using namespace msm;
 
@@ -659,6 +660,22 @@ size_t msm_set_engine_cache_limit(size_t bytes) {
   PoolStats st;  // a lowered limit trims the engines already idle
   PoolRegistry::get().visit(st, false);
   return prev;
+}
+
+int msm_register_host_table(int group, const void *rows, size_t nrows) {
+  if ((group != 1 && group != 2) || !rows || !nrows) return fail(MSM_E_ARG, "bad group / rows");
+  try {
+    if (group == 1) register_host_table<1>(rows, nrows);
+    else register_host_table<2>(rows, nrows);
+    return MSM_OK;
+  } catch (const std::exception &e) {
+    return fail(MSM_E_HIP, e.what());
+  }
+}
+
+int msm_unregister_host_table(const void *rows) {
+  if (!rows) return fail(MSM_E_ARG, "null rows");
+  return TableRegistry::get().remove(rows) ? MSM_OK : fail(MSM_E_ARG, "table not registered");
 }
 
 int msm_device_count(void) {

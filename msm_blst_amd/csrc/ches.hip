@@ -205,7 +205,7 @@ template struct ScanReducer<MSM_GROUP>;
 // then a dense scatter into 2 windows of 2^s slots), followed by the dense
 // 2-window ScanReducer and a 2^s Horner step on the host.
 template <int G>
-void WeightedReducer<G>::plan(const std::vector<uint32_t> &w, const std::vector<uint32_t> &win, int nwin) {
+void WeightedReducer<G>::plan(const std::vector<uint32_t> &w, const std::vector<uint32_t> &win, int nwin, int c0) {
   typedef typename FieldOf<G>::F F;
   if (nwin < 1 || (!win.empty() && win.size() != w.size())) throw std::runtime_error("WeightedReducer: bad windows");
   bsize_ = w.size();
@@ -248,7 +248,8 @@ void WeightedReducer<G>::plan(const std::vector<uint32_t> &w, const std::vector<
     return e ? std::max(2, std::min(64, atoi(e))) : 0;
   }();
   const size_t lane_items = idx.size() * (G == 2 ? 2 : 1);  // G2 segment sums run on lane pairs
-  int C = C0env ? C0env : lane_items >= ((size_t)3 << 19) ? 8 : lane_items >= ((size_t)600 << 10) ? 4 : 2;
+  int C = C0env ? C0env : c0 ? c0 : lane_items >= ((size_t)3 << 19) ? 8 : lane_items >= ((size_t)600 << 10) ? 4 : 2;
+  c0_ = C;
   while (true) {
     std::vector<uint32_t> st, nseg;
     size_t k = 0;
@@ -456,7 +457,7 @@ void WeightedReducer<G>::launch_head_slot(hipStream_t s, const void *Sbuf, int s
 }
 
 template <int G>
-void WeightedReducer<G>::launch_tail_group(hipStream_t s, int set, int nmsm) {
+void WeightedReducer<G>::launch_tail_group(hipStream_t s, int set, int nmsm, bool coop) {
   typedef typename FieldOf<G>::F F;
   const size_t L = nout_.size();
   const Xyzz<F> *src = part_[set][0].as<Xyzz<F>>();
@@ -470,7 +471,7 @@ void WeightedReducer<G>::launch_tail_group(hipStream_t s, int set, int nmsm) {
     MSM_HIP_CHECK(hipGetLastError());
     src = dst;
   }
-  dense_[set].launch(s, dense_buf_[set].p, 2 * nwin_ * nmsm, 1 << sbits_, false);
+  dense_[set].launch(s, dense_buf_[set].p, 2 * nwin_ * nmsm, 1 << sbits_, coop);
 }
 
 template <int G>
@@ -602,6 +603,16 @@ void Ches<G>::plan_buckets(size_t n) {
     for (int k = 1; k <= small_; ++k) w.push_back((uint32_t)B_[k]);
   if (w.size() >= (1u << 24)) throw std::runtime_error("CHES bucket space exceeds 24-bit indices");
   red_.plan(w);
+  static const int bc_env = [] {  // A/B knob: the batch reducer's level-0 chunk (0: red_'s)
+    const char *e = getenv("MSM_BATCH_L0_CHUNK");
+    return e ? std::max(0, std::min(64, atoi(e))) : 8;
+  }();
+  if (bc_env && red_.level0_chunk() != bc_env) {
+    bred_.plan(w, bc_env);
+    batch_red_ = &bred_;
+  } else {
+    batch_red_ = &red_;
+  }
 }
 
 // Accumulation lanes of a batch (run_batch): 3 (G1) or 2 (G2) when one
@@ -805,7 +816,7 @@ void Ches<G>::accumulate_l0(hipStream_t s, int set, int r, int bset, const void 
   typedef typename FieldOf<G>::F F;
   const size_t NB = bucket_count();
   ChesFrontSet &f = fs_[set];
-  const typename WeightedReducer<G>::HeadArgs a = red_.head_args(gset, slot);
+  const typename WeightedReducer<G>::HeadArgs a = batch_red_->head_args(gset, slot);
   const AccSched S = f.sort.sched(f.order.as<uint32_t>(), f.sorted.as<uint32_t>(), r, NB);
   const AffP<F> *T = table ? static_cast<const AffP<F> *>(table) : table_.as<AffP<F>>();
   // lanes: one per bucket / output (G1), two (G2 lane pairs)
@@ -863,6 +874,13 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
   DeviceGuard g(dev_);
   if (stride < 32) throw std::runtime_error("CHES scalars must be 32-byte strings");
   if (nseg < 1) throw std::runtime_error("run_jobs: no segments");
+  WeightedReducer<G> &red = *batch_red_;
+  // the dense stage of the batch's LAST group runs its adds over 4 waves each
+  // (nothing else left to overlap; MSM_TAIL_COOP=0: one lane per add throughout)
+  static const bool tail_coop = [] {
+    const char *e = getenv("MSM_TAIL_COOP");
+    return !e || atoi(e) != 0;
+  }();
   // jobs k = set (k / nseg), segment (k % nseg); every loop below runs over jobs
   const size_t count = nsets * nseg;
   if (count == 0) return;
@@ -906,7 +924,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
   }
   // one pinned read-back slot per MSM of the batch: the host never waits inside
   // the issue loop, so MSM k+1's front is queued while MSM k still accumulates
-  const size_t ob = red_.out_bytes();  // a group's read-back lands contiguously
+  const size_t ob = red.out_bytes();  // a group's read-back lands contiguously
   // reduction groups of R <= kGroup MSMs (balanced sizes), alternating between
   // the two reducer sets / tail streams
   static const size_t group_max = [] {  // A/B knob: MSMs per reduction group (default kGroup)
@@ -965,7 +983,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
   // launches, ~1 ms beside the accumulations: with 2 sets group q + 2 waited
   // for it, profiles/r04_batch_trace_2p17.txt)
   const int nfr = nl >= 2 ? kFrontsMax : kFronts, nred = nl >= 2 ? 4 : 2;
-  for (int t = 0; t < nred; ++t) red_.ensure_group(t, (int)group_max);
+  for (int t = 0; t < nred; ++t) red.ensure_group(t, (int)group_max);
   // front sets sized for a whole front group (the sort's scan scratch too): run
   // one sort of fg_max sets per set before the loop if they are not yet sized
   // (fg_max dummy sets of all-zero scalars, outside the batch timing)
@@ -1131,12 +1149,12 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
         accumulate(L, (int)(g % nfr), (int)(k - fgb[g]), bset, job_table(k));
         if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k + 1], L));
         MSM_HIP_CHECK(hipEventRecord(eva[k], L));
-        red_.launch_head_slot(L, buckets_[bset].p, gset, slot);
+        red.launch_head_slot(L, buckets_[bset].p, gset, slot);
         MSM_HIP_CHECK(hipEventRecord(evh[k], L));
         if ((size_t)slot + 1 == R || k + 1 == count) {  // the group's level 0s are done on both lanes
           for (int d = 0; d < nl && d <= slot; ++d) MSM_HIP_CHECK(hipStreamWaitEvent(ts, evh[k - d], 0));
-          red_.launch_tail_group(ts, gset, slot + 1);
-          red_.copy_out_group(ts, gset, slot + 1, (uint8_t *)host_out_ + (k - slot) * ob);
+          red.launch_tail_group(ts, gset, slot + 1, tail_coop && k + 1 == count);
+          red.copy_out_group(ts, gset, slot + 1, (uint8_t *)host_out_ + (k - slot) * ob);
           MSM_HIP_CHECK(hipEventRecord(evt[q], ts));
         }
       }
@@ -1159,8 +1177,8 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
     if (pslot + 1 != R && p + 1 != count) return;
     hipStream_t ts = tails_[pq % 2];
     MSM_HIP_CHECK(hipStreamWaitEvent(ts, evh[p], 0));
-    red_.launch_tail_group(ts, (int)(pq % 2), (int)pslot + 1);
-    red_.copy_out_group(ts, (int)(pq % 2), (int)pslot + 1, (uint8_t *)host_out_ + (p - pslot) * ob);
+    red.launch_tail_group(ts, (int)(pq % 2), (int)pslot + 1, tail_coop && p + 1 == count);
+    red.copy_out_group(ts, (int)(pq % 2), (int)pslot + 1, (uint8_t *)host_out_ + (p - pslot) * ob);
     MSM_HIP_CHECK(hipEventRecord(evt[pq], ts));
   };
   auto l0_set_free = [&](size_t p) {  // level 0 of MSM p may write its reducer set
@@ -1191,7 +1209,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
   if (fuse && nl < 2) {  // level 0 of the last MSM, alone
     const size_t p = count - 1;
     l0_set_free(p);
-    red_.launch_head_slot(s, buckets_[p % kBSets].p, (int)((p / R) % 2), (int)(p % R));
+    red.launch_head_slot(s, buckets_[p % kBSets].p, (int)((p / R) % 2), (int)(p % R));
     MSM_HIP_CHECK(hipEventRecord(evh[p], s));
     l0_group_tail(p);
   }
@@ -1209,11 +1227,11 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
       if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k + 1], s));
       MSM_HIP_CHECK(hipEventRecord(eva[k], s));
       MSM_HIP_CHECK(hipStreamWaitEvent(ts, eva[k], 0));
-      red_.launch_head_slot(ts, buckets_[bset].p, gset, slot);
+      red.launch_head_slot(ts, buckets_[bset].p, gset, slot);
       MSM_HIP_CHECK(hipEventRecord(evh[k], ts));
       if ((size_t)slot + 1 == R || k + 1 == count) {  // the reduction group's last MSM
-        red_.launch_tail_group(ts, gset, slot + 1);
-        red_.copy_out_group(ts, gset, slot + 1, (uint8_t *)host_out_ + (k - slot) * ob);
+        red.launch_tail_group(ts, gset, slot + 1, tail_coop && k + 1 == count);
+        red.copy_out_group(ts, gset, slot + 1, (uint8_t *)host_out_ + (k - slot) * ob);
       }
     }
   }
@@ -1228,7 +1246,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
   MSM_HIP_CHECK(hipStreamSynchronize(fstream_));  // three lanes: the group read-backs ran on the front stream
   // the per-MSM host Horner (~20 us each) over the host worker threads: with
   // one reduction group per batch every combine runs after the last tail
-  auto combine_k = [&](size_t k) { outs[k] = red_.combine((const uint8_t *)host_out_ + k * ob)[0]; };
+  auto combine_k = [&](size_t k) { outs[k] = red.combine((const uint8_t *)host_out_ + k * ob)[0]; };
   if (count >= 4) {
     WorkerPool::get().parallel_for(count, combine_k);
   } else {

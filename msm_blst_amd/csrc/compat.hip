@@ -10,6 +10,7 @@
 // WeightedReducer for sum_b w_b S_b.  Reference weights: bucket_set_ascend[idx]
 // (d_CHES), the bucket value itself (noindexhash, BGMW95).
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -19,6 +20,7 @@
 #include "hoststage.hpp"
 #include "pair_kernels.hpp"
 #include "pool.hpp"
+#include "table_registry.hpp"
 
 #ifndef MSM_GROUP
 #error "define MSM_GROUP (1 or 2)"
@@ -65,7 +67,7 @@ struct EntryMsmState {
   size_t device_bytes() const {  // device buffers + pinned staging (the pool's idle budget counts both)
     size_t b = hkv.bytes + hring.bytes + hbx.bytes;
     for (const DevBuf *d : {&pts, &keys, &vals, &sorted, &counts, &offsets, &order, &buckets, &xfer, &bx}) b += d->bytes;
-    return b;
+    return b + sort.device_bytes() + red.device_bytes();
   }
 };
 
@@ -84,8 +86,8 @@ static void plan_if_changed(EntryMsmState<G> &S, const uint32_t *w, size_t nb) {
   S.red.plan(S.planned);
 }
 
-template <int G>
-static void entry_msm_back(EntryMsmState<G> &S, hipStream_t s, void *ret, size_t ne, size_t nb,
+template <int G, class PT>
+static void entry_msm_back(EntryMsmState<G> &S, hipStream_t s, const PT *pts, void *ret, size_t ne, size_t nb,
                            const uint32_t *weights, void *buckets_out, bool pinned_export);
 
 template <int G>
@@ -118,13 +120,13 @@ void entry_msm(void *ret, const void *pts_blst, size_t npts, const uint32_t *key
     MSM_HIP_CHECK(hipMemcpyAsync(S.keys.p, keys, ne * 4, hipMemcpyHostToDevice, s));
     MSM_HIP_CHECK(hipMemcpyAsync(S.vals.p, vals, ne * 4, hipMemcpyHostToDevice, s));
   }
-  entry_msm_back<G>(S, s, ret, ne, nb, weights, buckets_out, false);
+  entry_msm_back<G>(S, s, S.pts.template as<Aff<F>>(), ret, ne, nb, weights, buckets_out, false);
 }
 
 // sort + accumulate + (bucket export) + weighted reduction of the entries in
-// S.keys / S.vals over the points in S.pts
-template <int G>
-static void entry_msm_back(EntryMsmState<G> &S, hipStream_t s, void *ret, size_t ne, size_t nb,
+// S.keys / S.vals over the point rows pts (S.pts, or a registered table)
+template <int G, class PT>
+static void entry_msm_back(EntryMsmState<G> &S, hipStream_t s, const PT *pts, void *ret, size_t ne, size_t nb,
                            const uint32_t *weights, void *buckets_out, bool pinned_export) {
   typedef typename FieldOf<G>::F F;
   typedef typename HostField<G>::F HF;
@@ -135,8 +137,7 @@ static void entry_msm_back(EntryMsmState<G> &S, hipStream_t s, void *ret, size_t
   S.buckets.ensure(nb * sizeof(Xyzz<F>));
   S.sort.run(s, S.keys.template as<uint32_t>(), S.vals.template as<uint32_t>(), ne, (uint32_t)nb, S.sorted.template as<uint32_t>(),
              S.counts.template as<uint32_t>(), S.offsets.template as<uint32_t>(), S.order.template as<uint32_t>());
-  launch_accumulate<G>(s, S.sort.sched(S.order.template as<uint32_t>(), S.sorted.template as<uint32_t>(), 0, nb),
-                       S.pts.template as<Aff<F>>(),
+  launch_accumulate<G>(s, S.sort.sched(S.order.template as<uint32_t>(), S.sorted.template as<uint32_t>(), 0, nb), pts,
                        S.buckets.template as<Xyzz<F>>(), nb);
   MSM_HIP_CHECK(hipGetLastError());
   plan_if_changed(S, weights, nb);
@@ -184,15 +185,51 @@ void entry_msm_ptrs(void *ret, const void *const *points, size_t ne, EntryFill f
     const size_t t0 = c * piece, t1 = std::min(ne, t0 + piece);
     fill(fill_ctx, t0, t1, hk + t0, hv + t0);
   });
+  // a registered table holding every pointed-to row: vals become row indices
+  // (sign bit kept) and no row is gathered (table_registry.hpp)
+  int dev = 0;
+  MSM_HIP_CHECK(hipGetDevice(&dev));
+  std::shared_ptr<HostTable> tab = TableRegistry::get().find(G, dev, points[0]);
+  if (tab) {
+    std::atomic<bool> outside{false};
+    const uint8_t *base = tab->base;
+    const size_t span = tab->nrows * psz;
+    WorkerPool::get().parallel_for((ne + piece - 1) / piece, [&](size_t c) {
+      const size_t t0 = c * piece, t1 = std::min(ne, t0 + piece);
+      for (size_t t = t0; t < t1; ++t) {
+        const size_t off = (size_t)(static_cast<const uint8_t *>(points[t]) - base);
+        if (off >= span || off % psz) {
+          outside.store(true, std::memory_order_relaxed);
+          return;
+        }
+        hv[t] = (uint32_t)(off / psz) | (hv[t] & 0x80000000u);
+      }
+    });
+    if (outside.load()) {  // back to entry indices (vals were t | sign) and the gather
+      WorkerPool::get().parallel_for((ne + piece - 1) / piece, [&](size_t c) {
+        const size_t t0 = c * piece, t1 = std::min(ne, t0 + piece);
+        for (size_t t = t0; t < t1; ++t) hv[t] = (uint32_t)t | (hv[t] & 0x80000000u);
+      });
+      tab.reset();
+    }
+  }
   S.keys.ensure(ne * 4);
   S.vals.ensure(ne * 4);
   S.sorted.ensure(ne * 4 + 64);  // + the accumulation's payload window
   MSM_HIP_CHECK(hipMemcpyAsync(S.keys.p, hk, ne * 4, hipMemcpyHostToDevice, s));
   MSM_HIP_CHECK(hipMemcpyAsync(S.vals.p, hv, ne * 4, hipMemcpyHostToDevice, s));
+  if (tab) {
+    entry_msm_back<G>(S, s, tab->rows.template as<AffP<F>>(), ret, ne, nb, weights, buckets_out, true);
+    return;
+  }
   // point rows: gathered chunk by chunk into a 4-slot pinned ring (the host
   // gather of chunk c + 1 overlaps the DMA of chunk c), converted on the device
+  // 4 slots of at most 32 MiB: the ring is 128 MiB of page-locked memory
+  // whatever ne (ne / 16 rows per slot kept ~300 MB / 600 MB pinned per pooled
+  // state for a 2^20 G1 / G2 tile); a 2^20 tile goes ~36 times
+  // around the ring
   constexpr int kSlots = 4;
-  const size_t chunk = std::min(ne, std::max<size_t>(((size_t)16 << 20) / psz, (ne + kSlots - 1) / kSlots / 4 + 1));
+  const size_t chunk = std::min(ne, ((size_t)32 << 20) / psz);
   S.hring.ensure(chunk * psz * kSlots);
   for (hipEvent_t &e : S.ring_ev)
     if (!e) MSM_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -215,7 +252,40 @@ void entry_msm_ptrs(void *ret, const void *const *points, size_t ne, EntryFill f
   hipLaunchKernelGGL(k_convert_points<G>, dim3(nblk(ne, 256)), dim3(256), 0, s, S.xfer.template as<uint64_t>(),
                      S.pts.template as<Aff<F>>(), ne);
   MSM_HIP_CHECK(hipGetLastError());
-  entry_msm_back<G>(S, s, ret, ne, nb, weights, buckets_out, true);
+  entry_msm_back<G>(S, s, S.pts.template as<Aff<F>>(), ret, ne, nb, weights, buckets_out, true);
+}
+
+template <int G>
+void register_host_table(const void *rows, size_t nrows) {
+  typedef typename FieldOf<G>::F F;
+  if (!rows || !nrows) throw std::runtime_error("empty table");
+  if (nrows >= (1ull << 31)) throw std::runtime_error("registered table exceeds 31-bit row indices");
+  auto t = std::make_shared<HostTable>();
+  MSM_HIP_CHECK(hipGetDevice(&t->device));
+  t->group = G;
+  t->base = static_cast<const uint8_t *>(rows);
+  t->nrows = nrows;
+  t->rows.ensure(nrows * sizeof(AffP<F>));
+  const size_t psz = 96 * G, chunk = std::min<size_t>(nrows, ((size_t)64 << 20) / psz);
+  hipStream_t s;
+  MSM_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  try {
+    DevBuf stage;
+    stage.ensure(chunk * psz);
+    for (size_t r0 = 0; r0 < nrows; r0 += chunk) {  // pageable caller rows, 64-MiB pieces
+      const size_t cnt = std::min(chunk, nrows - r0);
+      MSM_HIP_CHECK(hipMemcpyAsync(stage.p, t->base + r0 * psz, cnt * psz, hipMemcpyHostToDevice, s));
+      hipLaunchKernelGGL((k_convert_points<G, AffP<F>>), dim3(nblk(cnt, 256)), dim3(256), 0, s,
+                         stage.template as<uint64_t>(), t->rows.template as<AffP<F>>() + r0, cnt);
+      MSM_HIP_CHECK(hipGetLastError());
+      MSM_HIP_CHECK(hipStreamSynchronize(s));  // the stage is reused
+    }
+  } catch (...) {
+    (void)hipStreamDestroy(s);
+    throw;
+  }
+  MSM_HIP_CHECK(hipStreamDestroy(s));
+  TableRegistry::get().add(std::move(t));
 }
 
 // sum_i w_i buckets[i] for caller-filled blst xyzz buckets
@@ -249,5 +319,6 @@ template void entry_msm<MSM_GROUP>(void *, const void *, size_t, const uint32_t 
 template void weighted_bucket_sum<MSM_GROUP>(void *, const void *, size_t, const uint32_t *);
 template void entry_msm_ptrs<MSM_GROUP>(void *, const void *const *, size_t, EntryFill, void *, size_t,
                                         const uint32_t *, void *);
+template void register_host_table<MSM_GROUP>(const void *, size_t);
 
 }  // namespace msm

@@ -124,7 +124,7 @@ size_t Pippenger<G>::device_bytes() const {
   size_t b = stage_ ? stage_->pinned_bytes() : 0;
   for (const DevBuf *d : {&pts_, &buckets_[0], &buckets_[1], &tmp_, &scal_}) b += d->bytes;
   for (const ChesFrontSet &f : fs_) b += f.device_bytes();
-  return b;
+  return b + red_.device_bytes();
 }
 
 template <int G>

@@ -174,8 +174,10 @@ class WeightedReducer {
   typedef typename HostField<G>::F HF;
   static constexpr int NSETS = 4;  // buffer sets, allocated on first use (batch reduction groups rotate over them)
   // win[i] in [0, nwin): the window of bucket i (empty = all in window 0)
-  void plan(const std::vector<uint32_t> &w, const std::vector<uint32_t> &win, int nwin);
-  void plan(const std::vector<uint32_t> &w) { plan(w, {}, 1); }
+  // c0: level-0 chunk length (0: by plan size, see plan())
+  void plan(const std::vector<uint32_t> &w, const std::vector<uint32_t> &win, int nwin, int c0 = 0);
+  void plan(const std::vector<uint32_t> &w, int c0 = 0) { plan(w, {}, 1, c0); }
+  int level0_chunk() const { return c0_; }
   void launch_head(hipStream_t s, const void *S, int set);  // level 0 (reads S = xyzz[w.size()])
   // levels >= 1, dense, finalize; coop: see ScanReducer::launch
   void launch_tail(hipStream_t s, int set, bool coop = true);
@@ -195,6 +197,17 @@ class WeightedReducer {
   // set 0's sum_w 2^(c w) T_w (after launch_tail), waits
   hfp::Jac<HF> read_total(hipStream_t s, int c);
   size_t size() const { return bsize_; }
+  // device bytes held: plan tables, every buffer set (partials, dense slots and
+  // their ScanReducer buffers), the bit-phase read-back (engine pool budget)
+  size_t device_bytes() const {
+    size_t b = idx_.bytes + bfin_.bytes;
+    for (const DevBuf &d : starts_) b += d.bytes;
+    for (const DevBuf &d : bstarts_) b += d.bytes;
+    for (int t = 0; t < NSETS; ++t)
+      b += dense_buf_[t].bytes + part_[t][0].bytes + part_[t][1].bytes + dense_[t].buf[0].bytes +
+           dense_[t].buf[1].bytes + dense_[t].fin.bytes;
+    return b;
+  }
 
   void ensure_set(int set);  // allocate buffer set `set` for the current plan
 
@@ -213,7 +226,9 @@ class WeightedReducer {
     size_t nout;
   };
   HeadArgs head_args(int set, int slot);
-  void launch_tail_group(hipStream_t s, int set, int nmsm);          // levels >= 1, dense, finalize
+  // levels >= 1, dense, finalize; coop: the dense stage's adds over 4 waves each
+  // (shortest latency when nothing else runs, e.g. the last group of a batch)
+  void launch_tail_group(hipStream_t s, int set, int nmsm, bool coop = false);
   void copy_out_group(hipStream_t s, int set, int nmsm, void *host);  // nmsm * out_bytes()
 
  private:
@@ -221,7 +236,7 @@ class WeightedReducer {
   size_t bit_slots() const { return (size_t)2 * nwin_ * sbits_; }
   size_t bsize_ = 0, final_perm_off_ = 0, maxp_ = 1;
   size_t maxp1_ = 1;  // batch groups: partials per MSM in part_[.][1] (the odd tail levels)
-  int sbits_ = 1, nwin_ = 1;
+  int sbits_ = 1, nwin_ = 1, c0_ = 8;
   DevBuf idx_, dense_buf_[NSETS], part_[NSETS][2];
   std::vector<DevBuf> starts_;
   std::vector<size_t> nout_;
@@ -412,6 +427,15 @@ class Ches {
   DevBuf scal_;
   DevBuf prime_;  // target of the one-time stream priming launches (run_batch)
   WeightedReducer<G> red_;
+  // the batch's reducer: red_ when its level-0 chunk is 8, else bred_, the same
+  // weights planned with chunks of 8.  Small plans chunk level 0 by 2-4 for the
+  // synchronous MSM's latency; in a batch level 0 runs beside other lanes'
+  // accumulations while the grouped tail runs exposed after the last one, so
+  // the batch moves the adds into level 0 (2^17: the group tail's first segment
+  // level alone was 0.51 ms, profiles/r04_batch_trace_2p17_lanes3.txt).
+  // MSM_BATCH_L0_CHUNK=<2..64> overrides 8; =0 reuses red_.
+  WeightedReducer<G> bred_;
+  WeightedReducer<G> *batch_red_ = &red_;
   std::vector<hipEvent_t> ev_;
   hipStream_t tails_[kBSets] = {nullptr, nullptr}, fstream_ = nullptr, cstream_ = nullptr;  // batch streams (+ the caller's)
   hipEvent_t ev_tail_[kBSets] = {nullptr, nullptr};

@@ -133,3 +133,66 @@ def test_tile_bgmw95(env):
         ret = (ctypes.c_uint8 * (144 * G))()
         env.fn("blst_p{g}_tile_pippenger_BGMW95")(ret, ptrs, n * hb, vals, signs, buckets, qb)
         assert m.compress(G, bytes(ret)).hex() == run["bgmw95"] == run["pippenger"]
+
+
+def test_registered_table_tiles(env):
+    """msm_register_host_table: the driver's host table registered once, then the
+    method-2 tile (main_p1.cpp:249-291) ships row indices instead of gathering
+    rows -- same result, same buckets left filled (integrate over them), the
+    same for noindexhash and the BGMW95 tile over its registered table; a
+    pointer outside the registered rows falls back to the gather; after
+    unregistering, the gather path again."""
+    m, G, g, T, TB, B, H, v2i = env.m, env.G, env.g, env.T, env.TB, env.B, env.H, env.v2i
+    L = m.lib()
+    n, h, qe = g["n"], g["h"], g["q_exp"]
+    run = _runs(g)[0]
+    sc = m.gen_scalars(n, run["seed"])
+    nh = _std_digits(sc, n, qe, h)
+    signs = (ctypes.c_ubyte * (n * h))()
+    ptrs = (ctypes.c_void_p * (n * h))()
+    env.fn("blst_p{g}_construct_nh_scalars_nh_points")(nh, signs, ptrs, n * h, T, H)
+    ref_buckets = (ctypes.c_uint8 * (192 * G * len(B)))()
+    ret = (ctypes.c_uint8 * (144 * G))()
+    env.fn("blst_p{g}_tile_pippenger_d_CHES")(ret, ptrs, n * h, nh, signs, ref_buckets, B, v2i, len(B), 6)
+    assert L.msm_register_host_table(G, T, 3 * n * h) == 0, L.msm_last_error()
+    try:
+        for _ in range(2):
+            buckets = (ctypes.c_uint8 * (192 * G * len(B)))()
+            ret = (ctypes.c_uint8 * (144 * G))()
+            env.fn("blst_p{g}_tile_pippenger_d_CHES")(ret, ptrs, n * h, nh, signs, buckets, B, v2i, len(B), 6)
+            assert m.compress(G, bytes(ret)).hex() == run["pippenger"]
+            ret2 = (ctypes.c_uint8 * (144 * G))()
+            env.fn("blst_p{g}_integrate_buckets_accumulation_d_CHES")(ret2, buckets, B, len(B), 6)
+            assert m.compress(G, bytes(ret2)).hex() == run["pippenger"]
+        bk = (ctypes.c_uint8 * (192 * G * (B[len(B) - 1] + 1)))()
+        env.fn("blst_p{g}_tile_pippenger_d_CHES_noindexhash")(ret, ptrs, n * h, nh, signs, bk, B, len(B), 6)
+        assert m.compress(G, bytes(ret)).hex() == run["pippenger"]
+        # one entry pointing at a copy of its row outside the table: the gather path
+        moved = (ctypes.c_uint8 * (96 * G)).from_buffer_copy(ctypes.string_at(ptrs[7], 96 * G))
+        saved = ptrs[7]
+        ptrs[7] = ctypes.addressof(moved)
+        env.fn("blst_p{g}_tile_pippenger_d_CHES")(ret, ptrs, n * h, nh, signs, ref_buckets, B, v2i, len(B), 6)
+        assert m.compress(G, bytes(ret)).hex() == run["pippenger"]
+        ptrs[7] = saved
+        # BGMW95 over its own registered table
+        assert L.msm_register_host_table(G, TB, n * g["h_bgmw"]) == 0
+        qb, hb = g["q_exp_bgmw"], g["h_bgmw"]
+        vals = (ctypes.c_int * (n * hb))()
+        bsig = (ctypes.c_ubyte * (n * hb))()
+        bptr = (ctypes.c_void_p * (n * hb))()
+        d = (ctypes.c_int * hb)()
+        for i in range(n):
+            of.lib().or_bgmw_digits(d, ctypes.byref(sc, 32 * i), qb, hb)
+            for j in range(hb):
+                vals[i * hb + j] = abs(d[j])
+                bsig[i * hb + j] = 1 if d[j] < 0 else 0
+                bptr[i * hb + j] = ctypes.addressof(TB) + 96 * G * (i * hb + j)
+        bb = (ctypes.c_uint8 * (192 * G * ((1 << (qb - 1)) + 1)))()
+        env.fn("blst_p{g}_tile_pippenger_BGMW95")(ret, bptr, n * hb, vals, bsig, bb, qb)
+        assert m.compress(G, bytes(ret)).hex() == run["pippenger"]
+    finally:
+        assert L.msm_unregister_host_table(T) == 0
+        L.msm_unregister_host_table(TB)
+    assert L.msm_unregister_host_table(T) != 0  # not registered any more
+    env.fn("blst_p{g}_tile_pippenger_d_CHES")(ret, ptrs, n * h, nh, signs, ref_buckets, B, v2i, len(B), 6)
+    assert m.compress(G, bytes(ret)).hex() == run["pippenger"]
