@@ -14,5 +14,17 @@ namespace msm {
 struct AccSched {
   const uint32_t *order, *counts, *offsets, *wbase, *ipay, *sorted;
 };
+// Set r of a front group sorted in one pass (BucketSort with nsets > 1): its
+// schedule arrays start r nb (order, counts, offsets), r nw (wbase) and r ipay
+// (ipay) entries after set 0's; `sorted` is shared (offsets index it).
+struct AccStride {
+  uint64_t nb, nw, ipay;
+};
+#ifdef __HIPCC__
+__host__ __device__ inline AccSched acc_set(const AccSched &S, const AccStride &st, uint32_t r) {
+  return AccSched{S.order + r * st.nb, S.counts + r * st.nb,  S.offsets + r * st.nb,
+                  S.wbase + r * st.nw, S.ipay + r * st.ipay, S.sorted};
+}
+#endif
 
 }  // namespace msm

@@ -457,6 +457,17 @@ void WeightedReducer<G>::launch_head_slot(hipStream_t s, const void *Sbuf, int s
 }
 
 template <int G>
+void WeightedReducer<G>::launch_head_slots(hipStream_t s, const void *Sbuf, size_t sstride, int set, int slot0,
+                                           int nmsm) {
+  typedef typename FieldOf<G>::F F;
+  const bool only = nout_.size() == 1;  // level 0 is also the last level
+  const HeadArgs a = head_args(set, slot0);
+  launch_segsum<G>(s, reinterpret_cast<const Xyzz<F> *>(Sbuf), a.idx, a.starts, static_cast<Xyzz<F> *>(a.dst), a.nout,
+                   nmsm, sstride, only ? dense_slots() : maxp_);
+  MSM_HIP_CHECK(hipGetLastError());
+}
+
+template <int G>
 void WeightedReducer<G>::launch_tail_group(hipStream_t s, int set, int nmsm, bool coop) {
   typedef typename FieldOf<G>::F F;
   const size_t L = nout_.size();
@@ -811,6 +822,17 @@ void Ches<G>::accumulate(hipStream_t s, int set, int r, int bset, const void *ta
 }
 
 template <int G>
+void Ches<G>::accumulate_sets(hipStream_t s, int set, int R, int gb, const void *table) {
+  typedef typename FieldOf<G>::F F;
+  const size_t NB = bucket_count();
+  ChesFrontSet &f = fs_[set];
+  launch_accumulate_sets<G>(s, f.sort.sched(f.order.as<uint32_t>(), f.sorted.as<uint32_t>(), 0, NB), f.sort.stride(NB),
+                            table ? static_cast<const AffP<F> *>(table) : table_.as<AffP<F>>(),
+                            gbuckets_[gb].as<Xyzz<F>>(), NB, R);
+  MSM_HIP_CHECK(hipGetLastError());
+}
+
+template <int G>
 void Ches<G>::accumulate_l0(hipStream_t s, int set, int r, int bset, const void *table, int l0_bset, int gset,
                             int slot, int l0_last) {
   typedef typename FieldOf<G>::F F;
@@ -959,7 +981,12 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
     const char *e = getenv("MSM_FINE_BT");
     return e && atoi(e) == 256 ? 256 : 1024;
   }();
-  const size_t fg_max = !packed ? 1 : fg_env ? fg_env : nl >= 3 ? 4 : nl == 2 ? 2 : (size_t)kFrontGroupDefault;
+  static const bool acc_group_env = [] {  // accumulation groups (below); MSM_ACC_GROUP=0: per-MSM lanes
+    const char *e = getenv("MSM_ACC_GROUP");
+    return !e || atoi(e) != 0;
+  }();
+  const bool acc_groups = nl >= 2 && nseg == 1 && acc_group_env;
+  const size_t fg_max = !packed ? 1 : fg_env ? fg_env : acc_groups ? 4 : nl >= 3 ? 4 : nl == 2 ? 2 : (size_t)kFrontGroupDefault;
   // front groups of 1, 1, 2, 4, then fg_max MSMs: the first accumulation
   // starts after one front, and each group's host sets (copied while the earlier
   // groups accumulate: a set copies in ~0.6 ms, an MSM accumulates in ~2.3) are
@@ -972,7 +999,10 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
   // every buffer the loop touches exists before the first launch (an allocation
   // inside the issue loop could synchronise the device)
   const size_t NB = bucket_count(), n = n_;
-  for (int b = 0; b < std::max(kBSets, nl); ++b) buckets_[b].ensure(NB * sizeof(Xyzz<typename FieldOf<G>::F>));
+  if (acc_groups)
+    for (DevBuf &b : gbuckets_) b.ensure(fg_max * NB * sizeof(Xyzz<typename FieldOf<G>::F>));
+  else
+    for (int b = 0; b < std::max(kBSets, nl); ++b) buckets_[b].ensure(NB * sizeof(Xyzz<typename FieldOf<G>::F>));
   // sized for kGroup whatever this batch's R: a later, larger batch must not
   // reallocate (a hipFree inside the pipelined region would synchronise it)
   // (both reducer sets, and both bucket sets, whatever this batch's length: a
@@ -1056,6 +1086,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
     bev_.push_back(e);
   }
   hipEvent_t *eva = bev_.data() + 1, *evh = eva + count, *evf = evh + count, *evc = evf + nfg, *evt = evc + nfg;
+  std::vector<size_t> prof_k;  // profiling: acc_ev_ pairs recorded (per MSM, or per accumulation group)
   MSM_HIP_CHECK(hipEventRecord(bev_[0], s));  // the batch starts after prior work on s
   MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, bev_[0], 0));
   MSM_HIP_CHECK(hipStreamWaitEvent(cstream_, bev_[0], 0));
@@ -1133,7 +1164,50 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
   // Three lanes (MSM_BATCH_LANES=3) add tails_[1] as a lane and move the group
   // tails to the front stream (the process has 4 hardware queues by default,
   // GPU_MAX_HW_QUEUES: one stream per queue).
-  if (nl >= 2) {
+  // Accumulation groups (small MSMs, one table for every job; MSM_ACC_GROUP=0
+  // selects the per-MSM lanes below): front group g's R_g sets accumulate in
+  // ONE launch (k_accumulate_sets, into bucket sets gbuckets_[g % 2]) on lane
+  // stream g % 2, then ONE level-0 launch per reduction group they touch; the
+  // reduction-group tails run on tails_[1].  A small MSM's own grid fills the
+  // chip's wave slots about one round deep and its last waves run with the chip
+  // half idle; side-by-side lanes left the accumulations at ~0.55 of the madd
+  // rate (2^17: 0.65 ms each, 1.5 running at a time; profiles/r05_small_trace.txt).
+  if (acc_groups) {
+    hipStream_t lane[2] = {s, tails_[0]}, ts = tails_[1];
+    for (size_t g = 0; g < nfg; ++g) {
+      copy_group(g + nsg);
+      front_group(g + nfr - 1);
+      const size_t k0 = fgb[g], k1 = fgb[g + 1];
+      const int gb = (int)(g & 1);
+      hipStream_t L = lane[gb];
+      MSM_HIP_CHECK(hipStreamWaitEvent(L, evf[g], 0));
+      if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k0], L));
+      accumulate_sets(L, (int)(g % nfr), (int)(k1 - k0), gb, job_table(k0));
+      if (prof) {
+        MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k0 + 1], L));
+        prof_k.push_back(k0);
+      }
+      for (size_t k = k0; k < k1; ++k) MSM_HIP_CHECK(hipEventRecord(eva[k], L));
+      for (size_t a = k0; a < k1;) {  // level 0, one launch per reduction group touched
+        const size_t q = a / R, b = std::min(k1, (q + 1) * R);
+        if (q >= (size_t)nred) MSM_HIP_CHECK(hipStreamWaitEvent(L, evt[q - nred], 0));  // reducer set free again
+        red.launch_head_slots(L, gbuckets_[gb].as<uint8_t>() + (a - k0) * NB * sizeof(Xyzz<typename FieldOf<G>::F>), NB,
+                              (int)(q % nred), (int)(a % R), (int)(b - a));
+        a = b;
+      }
+      for (size_t k = k0; k < k1; ++k) MSM_HIP_CHECK(hipEventRecord(evh[k], L));
+      for (size_t k = k0; k < k1; ++k) {  // tails of the reduction groups ending in [k0, k1)
+        if ((k + 1) % R != 0 && k + 1 != count) continue;
+        const size_t q = k / R, first = q * R;
+        MSM_HIP_CHECK(hipStreamWaitEvent(ts, evh[k], 0));  // this lane's level 0s of group q
+        if (k0 >= 1 && k0 - 1 >= first) MSM_HIP_CHECK(hipStreamWaitEvent(ts, evh[k0 - 1], 0));  // the other lane's
+        red.launch_tail_group(ts, (int)(q % nred), (int)(k - first + 1), tail_coop && k + 1 == count);
+        red.copy_out_group(ts, (int)(q % nred), (int)(k - first + 1), (uint8_t *)host_out_ + first * ob);
+        MSM_HIP_CHECK(hipEventRecord(evt[q], ts));
+      }
+    }
+  }
+  if (nl >= 2 && !acc_groups) {
     hipStream_t lane[3] = {s, tails_[0], tails_[1]}, ts = nl == 3 ? fstream_ : tails_[1];
     for (size_t g = 0; g < nfg; ++g) {
       copy_group(g + nsg);
@@ -1147,7 +1221,10 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
           MSM_HIP_CHECK(hipStreamWaitEvent(L, evt[q - nred], 0));
         if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k], L));
         accumulate(L, (int)(g % nfr), (int)(k - fgb[g]), bset, job_table(k));
-        if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k + 1], L));
+        if (prof) {
+          MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k + 1], L));
+          prof_k.push_back(k);
+        }
         MSM_HIP_CHECK(hipEventRecord(eva[k], L));
         red.launch_head_slot(L, buckets_[bset].p, gset, slot);
         MSM_HIP_CHECK(hipEventRecord(evh[k], L));
@@ -1198,7 +1275,10 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
                       (int)(((k - 1) / R) % 2), (int)((k - 1) % R), fuse == 2);
       else
         accumulate(s, (int)(g % nfr), (int)(k - fgb[g]), bset, job_table(k));
-      if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k + 1], s));
+      if (prof) {
+        MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k + 1], s));
+        prof_k.push_back(k);
+      }
       MSM_HIP_CHECK(hipEventRecord(eva[k], s));
       if (k >= 1) {
         MSM_HIP_CHECK(hipEventRecord(evh[k - 1], s));
@@ -1224,7 +1304,10 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
       if (l0_first && k >= 1) MSM_HIP_CHECK(hipStreamWaitEvent(s, evh[k - 1], 0));
       if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k], s));
       accumulate(s, (int)(g % nfr), (int)(k - fgb[g]), bset, job_table(k));
-      if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k + 1], s));
+      if (prof) {
+        MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k + 1], s));
+        prof_k.push_back(k);
+      }
       MSM_HIP_CHECK(hipEventRecord(eva[k], s));
       MSM_HIP_CHECK(hipStreamWaitEvent(ts, eva[k], 0));
       red.launch_head_slot(ts, buckets_[bset].p, gset, slot);
@@ -1253,9 +1336,9 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
     for (size_t k = 0; k < count; ++k) combine_k(k);
   }
   profile_ = prof;
-  if (prof) {  // average accumulation time over the batch (HIP events on stream s)
+  if (prof) {  // accumulation time per MSM over the batch (HIP events on the accumulation streams)
     float sum = 0;
-    for (size_t k = 0; k < count; ++k) {
+    for (size_t k : prof_k) {
       float ms;
       MSM_HIP_CHECK(hipEventSynchronize(acc_ev_[2 * k + 1]));
       MSM_HIP_CHECK(hipEventElapsedTime(&ms, acc_ev_[2 * k], acc_ev_[2 * k + 1]));
@@ -1263,7 +1346,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
     }
     times_ = PhaseTimes();
     times_.accumulate = sum / (float)count;
-    times_.accumulate_launches = (int)count;
+    times_.accumulate_launches = (int)prof_k.size();
   }
 }
 

@@ -11,12 +11,16 @@
 // (d_CHES), the bucket value itself (noindexhash, BGMW95).
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
 
 #include "ches_kernels.hpp"
 #include "engine.hpp"
+#include "heavy.hpp"
 #include "hoststage.hpp"
 #include "pair_kernels.hpp"
 #include "pool.hpp"
@@ -59,6 +63,7 @@ struct EntryMsmState {
   WeightedReducer<G> red;
   std::vector<uint32_t> planned;  // weights the reducer plan was built for
   PinnedBuf hkv, hring, hbx;      // pinned: keys + vals, the point-row ring, exported buckets
+  HeavyScratch heavy;             // heavy buckets split over several lanes (heavy.hpp)
   hipEvent_t ring_ev[4] = {};
   ~EntryMsmState() {
     for (hipEvent_t &e : ring_ev)
@@ -67,7 +72,7 @@ struct EntryMsmState {
   size_t device_bytes() const {  // device buffers + pinned staging (the pool's idle budget counts both)
     size_t b = hkv.bytes + hring.bytes + hbx.bytes;
     for (const DevBuf *d : {&pts, &keys, &vals, &sorted, &counts, &offsets, &order, &buckets, &xfer, &bx}) b += d->bytes;
-    return b + sort.device_bytes() + red.device_bytes();
+    return b + sort.device_bytes() + red.device_bytes() + heavy.device_bytes();
   }
 };
 
@@ -86,9 +91,38 @@ static void plan_if_changed(EntryMsmState<G> &S, const uint32_t *w, size_t nb) {
   S.red.plan(S.planned);
 }
 
+// MSM_TILE_TIMING=1: host-side phase times of each pointer-array tile call on
+// stderr (study knob for the per-call fixed cost)
+struct TileClock {
+  bool on;
+  std::chrono::steady_clock::time_point t0, t;
+  std::string line;
+  TileClock() {
+    static const bool env = [] {
+      const char *e = getenv("MSM_TILE_TIMING");
+      return e && atoi(e) != 0;
+    }();
+    on = env;
+    t0 = t = std::chrono::steady_clock::now();
+  }
+  void lap(const char *what) {
+    if (!on) return;
+    const auto n = std::chrono::steady_clock::now();
+    char b[64];
+    snprintf(b, sizeof b, " %s=%.3f", what, std::chrono::duration<double, std::milli>(n - t).count());
+    line += b;
+    t = n;
+  }
+  ~TileClock() {
+    if (on)
+      fprintf(stderr, "[tile] total=%.3f ms:%s\n",
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(), line.c_str());
+  }
+};
+
 template <int G, class PT>
 static void entry_msm_back(EntryMsmState<G> &S, hipStream_t s, const PT *pts, void *ret, size_t ne, size_t nb,
-                           const uint32_t *weights, void *buckets_out, bool pinned_export);
+                           const uint32_t *weights, void *buckets_out, bool pinned_export, TileClock *clk = nullptr);
 
 template <int G>
 void entry_msm(void *ret, const void *pts_blst, size_t npts, const uint32_t *keys, const uint32_t *vals, size_t ne,
@@ -127,7 +161,7 @@ void entry_msm(void *ret, const void *pts_blst, size_t npts, const uint32_t *key
 // S.keys / S.vals over the point rows pts (S.pts, or a registered table)
 template <int G, class PT>
 static void entry_msm_back(EntryMsmState<G> &S, hipStream_t s, const PT *pts, void *ret, size_t ne, size_t nb,
-                           const uint32_t *weights, void *buckets_out, bool pinned_export) {
+                           const uint32_t *weights, void *buckets_out, bool pinned_export, TileClock *clk) {
   typedef typename FieldOf<G>::F F;
   typedef typename HostField<G>::F HF;
   hfp::Jac<HF> out;
@@ -137,8 +171,10 @@ static void entry_msm_back(EntryMsmState<G> &S, hipStream_t s, const PT *pts, vo
   S.buckets.ensure(nb * sizeof(Xyzz<F>));
   S.sort.run(s, S.keys.template as<uint32_t>(), S.vals.template as<uint32_t>(), ne, (uint32_t)nb, S.sorted.template as<uint32_t>(),
              S.counts.template as<uint32_t>(), S.offsets.template as<uint32_t>(), S.order.template as<uint32_t>());
-  launch_accumulate<G>(s, S.sort.sched(S.order.template as<uint32_t>(), S.sorted.template as<uint32_t>(), 0, nb), pts,
-                       S.buckets.template as<Xyzz<F>>(), nb);
+  // the caller's entries as they come: the CHES top digit's few buckets hold
+  // n entries between them, so heavy buckets are split over several lanes
+  launch_accumulate_heavy<G>(s, S.sort.sched(S.order.template as<uint32_t>(), S.sorted.template as<uint32_t>(), 0, nb),
+                             pts, S.buckets.template as<Xyzz<F>>(), nb, S.heavy);
   MSM_HIP_CHECK(hipGetLastError());
   plan_if_changed(S, weights, nb);
   S.red.launch(s, S.buckets.p);
@@ -154,8 +190,11 @@ static void entry_msm_back(EntryMsmState<G> &S, hipStream_t s, const PT *pts, vo
       MSM_HIP_CHECK(hipMemcpyAsync(buckets_out, S.bx.p, nb * 192 * G, hipMemcpyDeviceToHost, s));
     }
   }
+  if (clk) clk->lap("enqueue");
   out = S.red.read(s);
+  if (clk) clk->lap("gpu");
   if (buckets_out && pinned_export) parallel_memcpy(buckets_out, S.hbx.p, nb * 192 * G);
+  if (clk) clk->lap("export");
   std::memcpy(ret, &out, sizeof out);
 }
 
@@ -172,10 +211,12 @@ void entry_msm_ptrs(void *ret, const void *const *points, size_t ne, EntryFill f
     return;
   }
   if (ne >= (1ull << 31)) throw std::runtime_error("entry MSM too large");
+  TileClock clk;
   auto lease = entry_state<G>();
   EntryMsmState<G> &S = **lease;
   hipStream_t s = lease->stream();
   MSM_HIP_CHECK(hipStreamSynchronize(s));  // the pinned buffers are free (no DMA of an earlier call pending)
+  clk.lap("lease");
   const size_t psz = 96 * G;
   // keys / vals: filled in parallel straight into pinned memory, one DMA each
   S.hkv.ensure(ne * 8);
@@ -185,6 +226,7 @@ void entry_msm_ptrs(void *ret, const void *const *points, size_t ne, EntryFill f
     const size_t t0 = c * piece, t1 = std::min(ne, t0 + piece);
     fill(fill_ctx, t0, t1, hk + t0, hv + t0);
   });
+  clk.lap("fill");
   // a registered table holding every pointed-to row: vals become row indices
   // (sign bit kept) and no row is gathered (table_registry.hpp)
   int dev = 0;
@@ -218,8 +260,9 @@ void entry_msm_ptrs(void *ret, const void *const *points, size_t ne, EntryFill f
   S.sorted.ensure(ne * 4 + 64);  // + the accumulation's payload window
   MSM_HIP_CHECK(hipMemcpyAsync(S.keys.p, hk, ne * 4, hipMemcpyHostToDevice, s));
   MSM_HIP_CHECK(hipMemcpyAsync(S.vals.p, hv, ne * 4, hipMemcpyHostToDevice, s));
+  clk.lap("rows");
   if (tab) {
-    entry_msm_back<G>(S, s, tab->rows.template as<AffP<F>>(), ret, ne, nb, weights, buckets_out, true);
+    entry_msm_back<G>(S, s, tab->rows.template as<AffP<F>>(), ret, ne, nb, weights, buckets_out, true, &clk);
     return;
   }
   // point rows: gathered chunk by chunk into a 4-slot pinned ring (the host
@@ -252,7 +295,8 @@ void entry_msm_ptrs(void *ret, const void *const *points, size_t ne, EntryFill f
   hipLaunchKernelGGL(k_convert_points<G>, dim3(nblk(ne, 256)), dim3(256), 0, s, S.xfer.template as<uint64_t>(),
                      S.pts.template as<Aff<F>>(), ne);
   MSM_HIP_CHECK(hipGetLastError());
-  entry_msm_back<G>(S, s, S.pts.template as<Aff<F>>(), ret, ne, nb, weights, buckets_out, true);
+  clk.lap("gather");
+  entry_msm_back<G>(S, s, S.pts.template as<Aff<F>>(), ret, ne, nb, weights, buckets_out, true, &clk);
 }
 
 template <int G>

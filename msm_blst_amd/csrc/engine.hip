@@ -105,7 +105,7 @@ template <int G>
 Pippenger<G>::~Pippenger() {
   for (auto &e : ev_) (void)hipEventDestroy(e);
   for (auto &e : bev_) (void)hipEventDestroy(e);
-  for (hipStream_t q : {fstream_, lane1_, tstream_})
+  for (hipStream_t q : {fstream_, lane1_, lane2_, tstream_})
     if (q) {
       (void)hipStreamSynchronize(q);
       (void)hipStreamDestroy(q);
@@ -122,9 +122,9 @@ Pippenger<G>::~Pippenger() {
 template <int G>
 size_t Pippenger<G>::device_bytes() const {
   size_t b = stage_ ? stage_->pinned_bytes() : 0;
-  for (const DevBuf *d : {&pts_, &buckets_[0], &buckets_[1], &tmp_, &scal_}) b += d->bytes;
+  for (const DevBuf *d : {&pts_, &buckets_[0], &buckets_[1], &buckets_[2], &tmp_, &scal_}) b += d->bytes;
   for (const ChesFrontSet &f : fs_) b += f.device_bytes();
-  return b + red_.device_bytes();
+  return b + red_.device_bytes() + (batch_red_ != &red_ ? bred_.device_bytes() : 0);
 }
 
 template <int G>
@@ -224,6 +224,16 @@ void Pippenger<G>::plan_reduction(int nbits) {
     win[k] = (uint32_t)w;
   }
   red_.plan(wt, win, W);
+  static const int bc_env = [] {  // A/B knob: the batch reducer's level-0 chunk (0: red_'s)
+    const char *e = getenv("MSM_PIP_L0_CHUNK");
+    return e ? std::max(0, std::min(64, atoi(e))) : 8;
+  }();
+  if (bc_env && red_.level0_chunk() != bc_env) {
+    bred_.plan(wt, win, W, bc_env);
+    batch_red_ = &bred_;
+  } else {
+    batch_red_ = &red_;
+  }
   red_W_ = W;
   red_tcl_ = tcl;
 }
@@ -283,20 +293,36 @@ void Pippenger<G>::run_batch(hipStream_t s, const uint8_t *d_scalars, size_t str
   const int W = (nbits + 1 + c_ - 1) / c_;
   const size_t NT = (size_t)W << (c_ - 1);
   plan_reduction(nbits);
+  WeightedReducer<G> &red = *batch_red_;
   if (!fstream_) {
     int least = 0, greatest = 0;
     MSM_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
     MSM_HIP_CHECK(hipStreamCreateWithPriority(&fstream_, hipStreamNonBlocking, greatest));
     MSM_HIP_CHECK(hipStreamCreateWithFlags(&lane1_, hipStreamNonBlocking));
+    MSM_HIP_CHECK(hipStreamCreateWithFlags(&lane2_, hipStreamNonBlocking));
     MSM_HIP_CHECK(hipStreamCreateWithFlags(&tstream_, hipStreamNonBlocking));
   }
+  // accumulation lanes: MSM k accumulates on lane k % nl into bucket set k % nl
+  // and runs its level 0 there; 2 (default) or 3 (MSM_PIP_LANES).  With three
+  // lanes the group tails move to the front stream (the process has 4 hardware
+  // queues, GPU_MAX_HW_QUEUES: one stream per queue).
+  static const int nl = [] {
+    const char *e = getenv("MSM_PIP_LANES");
+    return e ? std::max(1, std::min(3, atoi(e))) : 2;
+  }();
+  // the dense stage of the batch's last group over 4 waves per add (nothing left
+  // to overlap it with; MSM_TAIL_COOP=0: one lane per add)
+  static const bool tail_coop = [] {
+    const char *e = getenv("MSM_TAIL_COOP");
+    return !e || atoi(e) != 0;
+  }();
   // groups of R <= kGroup MSMs share one reduction tail (WeightedReducer batch groups)
   static const size_t group_max = [] {  // A/B knob: MSMs per reduction group
     const char *e = getenv("MSM_PIP_GROUP");
     return (size_t)(e ? std::max(1, std::min(32, atoi(e))) : kGroup);
   }();
   const size_t ngroups = (count + group_max - 1) / group_max, R = (count + ngroups - 1) / ngroups;
-  const size_t ob = red_.out_bytes();
+  const size_t ob = red.out_bytes();
   if (host_out_bytes_ < count * ob) {
     if (host_out_) (void)hipHostFree(host_out_);
     host_out_ = nullptr;
@@ -307,8 +333,8 @@ void Pippenger<G>::run_batch(hipStream_t s, const uint8_t *d_scalars, size_t str
   }
   // every buffer the pipeline touches exists before its first launch (an
   // allocation inside the issue loop would synchronise the device)
-  for (DevBuf &b : buckets_) b.ensure(NT * sizeof(Xyzz<F>));
-  for (int t = 0; t < kRedSets; ++t) red_.ensure_group(t, (int)group_max);
+  for (int b = 0; b < nl; ++b) buckets_[b].ensure(NT * sizeof(Xyzz<F>));
+  for (int t = 0; t < kRedSets; ++t) red.ensure_group(t, (int)group_max);
   for (int f = 0; f < kFronts; ++f)
     if (fs_[f].sorted.bytes < (size_t)W * n_ * 4 + 64) front(s, d_scalars, stride, nbits, nullptr, fs_[f]);
   MSM_HIP_CHECK(hipStreamSynchronize(s));
@@ -319,42 +345,42 @@ void Pippenger<G>::run_batch(hipStream_t s, const uint8_t *d_scalars, size_t str
   }
   hipEvent_t *evf = bev_.data() + 1, *eva = evf + count, *evh = eva + count, *evt = evh + count;
   MSM_HIP_CHECK(hipEventRecord(bev_[0], s));
-  for (hipStream_t q : {fstream_, lane1_, tstream_}) MSM_HIP_CHECK(hipStreamWaitEvent(q, bev_[0], 0));
+  for (hipStream_t q : {fstream_, lane1_, lane2_, tstream_}) MSM_HIP_CHECK(hipStreamWaitEvent(q, bev_[0], 0));
   auto front_k = [&](size_t k) {
     if (k >= count) return;
     if (k >= (size_t)kFronts) MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, eva[k - kFronts], 0));  // front set free
     front(fstream_, d_scalars + k * set_stride, stride, nbits, nullptr, fs_[k % kFronts]);
     MSM_HIP_CHECK(hipEventRecord(evf[k], fstream_));
   };
-  hipStream_t lane[2] = {s, lane1_};
+  hipStream_t lane[3] = {s, lane1_, lane2_}, ts = nl == 3 ? fstream_ : tstream_;
   for (size_t k = 0; k + 1 < (size_t)kFronts; ++k) front_k(k);
   for (size_t k = 0; k < count; ++k) {
     front_k(k + kFronts - 1);
-    hipStream_t L = lane[k & 1];
+    hipStream_t L = lane[k % nl];
     const size_t q = k / R;
     const int slot = (int)(k % R), gset = (int)(q % kRedSets);
     MSM_HIP_CHECK(hipStreamWaitEvent(L, evf[k], 0));
-    if (q >= (size_t)kRedSets && slot < 2)  // reducer set q % kRedSets free again (tail q - kRedSets)
+    if (q >= (size_t)kRedSets && slot < nl)  // reducer set q % kRedSets free again (tail q - kRedSets)
       MSM_HIP_CHECK(hipStreamWaitEvent(L, evt[q - kRedSets], 0));
-    accumulate(L, nbits, fs_[k % kFronts], buckets_[k & 1]);  // bucket set k % 2: lane k % 2 only, in order
+    accumulate(L, nbits, fs_[k % kFronts], buckets_[k % nl]);  // bucket set k % nl: lane k % nl only, in order
     MSM_HIP_CHECK(hipEventRecord(eva[k], L));
-    red_.launch_head_slot(L, buckets_[k & 1].p, gset, slot);
+    red.launch_head_slot(L, buckets_[k % nl].p, gset, slot);
     MSM_HIP_CHECK(hipEventRecord(evh[k], L));
     if ((size_t)slot + 1 == R || k + 1 == count) {
-      for (int d = 0; d < 2 && d <= slot; ++d) MSM_HIP_CHECK(hipStreamWaitEvent(tstream_, evh[k - d], 0));
-      red_.launch_tail_group(tstream_, gset, slot + 1);
-      red_.copy_out_group(tstream_, gset, slot + 1, (uint8_t *)host_out_ + (k - slot) * ob);
-      MSM_HIP_CHECK(hipEventRecord(evt[q], tstream_));
+      for (int d = 0; d < nl && d <= slot; ++d) MSM_HIP_CHECK(hipStreamWaitEvent(ts, evh[k - d], 0));
+      red.launch_tail_group(ts, gset, slot + 1, tail_coop && k + 1 == count);
+      red.copy_out_group(ts, gset, slot + 1, (uint8_t *)host_out_ + (k - slot) * ob);
+      MSM_HIP_CHECK(hipEventRecord(evt[q], ts));
     }
   }
   // the host Horner of group q overlaps the GPU work of later groups
   for (size_t q = 0; q * R < count; ++q) {
     MSM_HIP_CHECK(hipEventSynchronize(evt[q]));
     for (size_t k = q * R; k < std::min(count, (q + 1) * R); ++k)
-      outs[k] = red_.combine_windows((const uint8_t *)host_out_ + k * ob, c_);
+      outs[k] = red.combine_windows((const uint8_t *)host_out_ + k * ob, c_);
   }
   // the caller's stream observes completion of every stream of the batch
-  for (hipStream_t q : {fstream_, lane1_, tstream_}) {
+  for (hipStream_t q : {fstream_, lane1_, lane2_, tstream_}) {
     MSM_HIP_CHECK(hipEventRecord(bev_[0], q));
     MSM_HIP_CHECK(hipStreamWaitEvent(s, bev_[0], 0));
   }

@@ -89,6 +89,8 @@ struct BucketSort {
                     ipay.as<uint32_t>() + set * ipay_stride,
                     sorted};
   }
+  // the per-set offsets between consecutive sets of one multi-set sort
+  AccStride stride(size_t nb) const { return AccStride{nb, groups(nb), ipay_stride}; }
   // keys[ne] (bucket < nb or 0xffffffff), vals[ne]; outputs sized ne / nb.
   // nsets > 1: nsets independent sorts in the same launches -- inputs at
   // keys/vals + r ne, outputs counts/offsets/order + r nb (offsets index the one
@@ -218,6 +220,9 @@ class WeightedReducer {
   // launch beside an accumulation costs it time).
   void ensure_group(int set, int nmsm);
   void launch_head_slot(hipStream_t s, const void *S, int set, int slot);
+  // level 0 of nmsm consecutive MSMs (slots slot0 .. slot0 + nmsm - 1 of set
+  // `set`) in one launch; MSM j's buckets at S + j sstride points
+  void launch_head_slots(hipStream_t s, const void *S, size_t sstride, int set, int slot0, int nmsm);
   // the operands launch_head_slot would pass to its k_segsum (level 0 into slot
   // `slot` of set `set`), for a caller that runs level 0 inside another grid
   struct HeadArgs {
@@ -310,12 +315,13 @@ class Pippenger {
   PhaseTimes times_;
   static constexpr int kFronts = 5, kGroup = 8, kRedSets = 4;
   ChesFrontSet fs_[kFronts];  // digit/sort outputs: fs_[0] for run(), all of them for run_batch()
-  DevBuf pts_, buckets_[2], tmp_, scal_;
+  DevBuf pts_, buckets_[3], tmp_, scal_;  // buckets: one set per batch lane
   std::unique_ptr<HostStager> stage_;  // run_host: uploads from the caller's pageable memory
   hipStream_t up_ = nullptr;  // run_host: point upload stream
   hipEvent_t ev_up_ = nullptr, ev_s_ = nullptr;
   // run_batch: front stream, second accumulation lane, tail stream; events; read-back slots
-  hipStream_t fstream_ = nullptr, lane1_ = nullptr, tstream_ = nullptr;
+  // run_batch streams: fronts, lanes 1 and 2 (lane 0 is the caller's), tails
+  hipStream_t fstream_ = nullptr, lane1_ = nullptr, lane2_ = nullptr, tstream_ = nullptr;
   std::vector<hipEvent_t> bev_;
   void *host_out_ = nullptr;
   size_t host_out_bytes_ = 0;
@@ -325,6 +331,12 @@ class Pippenger {
   void plan_reduction(int nbits);  // reducer plan for this window layout (built once)
   void back(hipStream_t s, int nbits, hfp::Jac<HF> *out);  // accumulate + reduce + read-back (fs_[0])
   WeightedReducer<G> red_;
+  // run_batch's reducer: the same weights with level-0 chunks of 8 when red_
+  // (planned for the synchronous MSM's latency) chunks by less -- in a batch
+  // level 0 runs beside the other lane's accumulation, the grouped tail beside
+  // later MSMs (MSM_PIP_L0_CHUNK=<2..64> overrides, 0 reuses red_)
+  WeightedReducer<G> bred_;
+  WeightedReducer<G> *batch_red_ = &red_;
   int red_W_ = 0, red_tcl_ = -1;  // window count / top copies the reducer plan was built for
   // log2 of the top window's bucket copies (k_digits): 2^topbits digit values
   // spread over its 2^(c-1) slots
@@ -451,6 +463,10 @@ class Ches {
   // accumulation of scalar set r of front set `set` into bucket set bset
   // (table: the table_ of this engine, or of a segment's engine in run_jobs)
   void accumulate(hipStream_t s, int set, int r, int bset, const void *table = nullptr);
+  // accumulation group: sets 0 .. R-1 of front set `set` in one launch into
+  // the R consecutive bucket sets of gbuckets_[gb]
+  void accumulate_sets(hipStream_t s, int set, int R, int gb, const void *table);
+  DevBuf gbuckets_[2];  // accumulation groups: two lanes x kFrontGroup bucket sets
   // batch: accumulation as above in the same grid as level 0 of the MSM whose
   // buckets are in l0_bset, into reducer set gset / slot (k_accumulate_l0)
   void accumulate_l0(hipStream_t s, int set, int r, int bset, const void *table, int l0_bset, int gset, int slot,

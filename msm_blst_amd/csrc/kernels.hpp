@@ -304,6 +304,18 @@ __global__ void __launch_bounds__(256, MSM_ACC_WAVES)
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t < nbuckets) accumulate_bucket<G>(S, pts, buckets, t);
 }
+// The accumulations of a front group's R sets in ONE grid (blockIdx.y = set r,
+// buckets of set r at r nbuckets): a small MSM's one-lane-per-bucket grid fills
+// the chip's wave slots only ~1 round deep and its last, shortest waves run
+// with the chip half idle; R sets in one dispatch keep it full until the
+// group's last round (Ches::run_jobs, accumulation groups).
+template <int G, class PT>
+__global__ void __launch_bounds__(256, MSM_ACC_WAVES)
+    k_accumulate_sets(const AccSched S, const AccStride st, const PT *__restrict__ pts,
+                      Xyzz<typename FieldOf<G>::F> *__restrict__ buckets, size_t nbuckets) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < nbuckets) accumulate_bucket<G>(acc_set(S, st, blockIdx.y), pts, buckets + blockIdx.y * nbuckets, t);
+}
 
 // xyzz -> blst Jacobian (X*ZZ, Y*ZZZ, ZZ)  (ref ec_ops.h:771-777), canonical blst Montgomery
 // (one lane per window, 64-thread blocks: the bound lets G2 keep every operand

@@ -173,6 +173,15 @@ __global__ void __launch_bounds__(256)
   if (t < 2 * nbuckets) accumulate_pair(S, pts, buckets, t);  // whole pairs only: 2 nbuckets lanes
 }
 
+// k_accumulate_sets (kernels.hpp) for G2: R sets in one grid, lane pairs
+template <class PT>
+__global__ void __launch_bounds__(256)
+    k_accumulate2p_sets(const AccSched S, const AccStride st, const PT *__restrict__ pts, Xyzz<Fp2> *__restrict__ buckets,
+                        size_t nbuckets) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < 2 * nbuckets) accumulate_pair(acc_set(S, st, blockIdx.y), pts, buckets + blockIdx.y * nbuckets, t);
+}
+
 // k_segsum (ches_kernels.hpp) for G2 with two lanes per output
 __device__ __forceinline__ void segsum_pair(const Xyzz<Fp2> *__restrict__ src, const uint32_t *__restrict__ idx,
                                             const uint32_t *__restrict__ starts, Xyzz<Fp2> *__restrict__ dst,
@@ -272,6 +281,18 @@ inline void launch_accumulate(hipStream_t s, const AccSched &S, const PT *pts, X
     hipLaunchKernelGGL((k_accumulate<G, PT>), dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, S, pts, buckets, nb);
   else
     hipLaunchKernelGGL((k_accumulate2p<PT>), dim3((unsigned)((2 * nb + 255) / 256)), dim3(256), 0, s, S, pts, buckets, nb);
+}
+// R sets of one front group (schedules S + r st, buckets at r nb), one launch
+template <int G, class PT>
+inline void launch_accumulate_sets(hipStream_t s, const AccSched &S, const AccStride &st, const PT *pts,
+                                   Xyzz<typename FieldOf<G>::F> *buckets, size_t nb, int R) {
+  if (!nb || R < 1) return;
+  if constexpr (G == 1)
+    hipLaunchKernelGGL((k_accumulate_sets<G, PT>), dim3((unsigned)((nb + 255) / 256), (unsigned)R), dim3(256), 0, s, S,
+                       st, pts, buckets, nb);
+  else
+    hipLaunchKernelGGL((k_accumulate2p_sets<PT>), dim3((unsigned)((2 * nb + 255) / 256), (unsigned)R), dim3(256), 0, s,
+                       S, st, pts, buckets, nb);
 }
 // nmsm > 1: the same segment sums for nmsm MSMs of a batch group in one launch
 template <int G>

@@ -95,6 +95,24 @@ def test_equal_points_doubling_branch(m):
     ctx.close()
 
 
+@pytest.mark.parametrize("method", ["ches", "bgmw"])
+def test_equal_points_doubling_branch_g2(m, method):
+    """G2 (lane-pair kernels): equal points with equal scalars -- every bucket add
+    takes the doubling branch of xyzz_madd, and equal bucket sums meet in the
+    reduction's pairwise adds (xyzz_add / the cooperative tail's doubling branch,
+    coop.hpp) -- vs the CPU oracle's naive sum."""
+    n = 64
+    ctx = m.CHESContext(2, 0, n_exp=8) if method == "ches" else m.BGMWContext(2, 0, n_exp=8)
+    p0 = bytes(m.fixed_points(2, 1))
+    ctx.build_table(p0 * n, n)
+    s0 = bytes(m.gen_scalars(1, 9))
+    got = m.compress(2, ctx.mult(s0 * n))
+    pts = (ctypes.c_uint8 * (192 * n)).from_buffer_copy(p0 * n)
+    sc = (ctypes.c_uint8 * (32 * n)).from_buffer_copy(s0 * n)
+    assert got.hex() == of.compress(2, of.msm(2, pts, sc, n, 255, "naive"))
+    ctx.close()
+
+
 @pytest.mark.parametrize("group,n_exp", [(1, 16), (2, 12)])
 def test_skewed_buckets_mixed_payload_layout(m, group, n_exp):
     """A quarter of the scalars equal: their digits pile into h buckets of n/4
@@ -218,18 +236,21 @@ print("FRONT_GROUPS_OK" if ok else "FRONT_GROUPS_MISMATCH")
 """
 
 
-def test_batch_front_groups_of_eight():
-    """The grouped-front path (digits + sort of up to 8 MSMs in one pass per
-    stage; not the default, engine.hpp kFrontGroupDefault) selected with
-    MSM_FRONT_GROUP=8, which the library reads once per process: a child
-    process runs batches of 17 (G1) and 9 (G2) distinct sets -- front groups
-    1, 1, 2, 4, 8, 1 -- from device and pinned host memory against the
-    synchronous MSMs."""
+@pytest.mark.parametrize("knobs", [{"MSM_FRONT_GROUP": "8"}, {"MSM_ACC_GROUP": "0"},
+                                   {"MSM_ACC_GROUP": "0", "MSM_BATCH_LANES": "2"}])
+def test_batch_front_groups_of_eight(knobs):
+    """Non-default small-MSM batch schedules, selected by knobs the library reads
+    once per process: MSM_FRONT_GROUP=8 (digits + sort of up to 8 MSMs in one
+    pass per stage, and accumulation groups of up to 8 sets in one launch:
+    front groups 1, 1, 2, 4, 8, 1); MSM_ACC_GROUP=0 (the per-MSM accumulation
+    lanes of round 4, three lanes / two lanes).  A child process runs batches
+    of 17 (G1) and 9 (G2) distinct sets from device and pinned host memory
+    against the synchronous MSMs."""
     import os
     import subprocess
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, MSM_FRONT_GROUP="8")
+    env = dict(os.environ, **knobs)
     r = subprocess.run([sys.executable, "-c", _FRONT_GROUP_SCRIPT, repo], capture_output=True, text=True, env=env,
                        timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]

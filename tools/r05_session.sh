@@ -18,6 +18,14 @@ for step in "$@"; do
     bench) timeout -k 10 600 python -u bench.py > $O/bench.json 2> $O/bench.err; rc=$?
            python3 tools/bench_summary.py $O/bench.json ;;
     shards) timeout -k 10 400 python -u tools/shard_study.py > $O/shards.txt 2> $O/shards.err; rc=$?; cat $O/shards.txt ;;
+    pip) timeout -k 10 500 python -u tools/pip_study.py --envs "MSM_PIP_L0_CHUNK=0 MSM_TAIL_COOP=0;MSM_PIP_L0_CHUNK=0;MSM_PIP_L0_CHUNK=8;MSM_PIP_L0_CHUNK=8 MSM_PIP_LANES=3;MSM_PIP_L0_CHUNK=4 MSM_PIP_LANES=3" > $O/pip.txt 2> $O/pip.err; rc=$?; cat $O/pip.txt ;;
+    shards_ab) timeout -k 10 500 python -u tools/shard_study.py --cfgs 20,19 > $O/shards_ab.txt 2> $O/shards_ab.err && MSM_BATCH_L0_CHUNK=0 MSM_TAIL_COOP=0 timeout -k 10 500 python -u tools/shard_study.py --cfgs 20,19 >> $O/shards_ab.txt 2>> $O/shards_ab.err; rc=$?; cat $O/shards_ab.txt ;;
+    trace) cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/trace -o run -- python3 $R/tools/r04_small_trace.py pb16 c17 > $O/trace.txt 2> $O/trace.err; rc=$?; cd $R
+           cat $O/trace.txt; python3 tools/batch_profile.py $O/trace/run_kernel_trace.csv > $O/trace_profile.txt; cat $O/trace_profile.txt ;;
+    shards_acc) timeout -k 10 300 python -u tools/shard_study.py --cfgs 20,19 > $O/shards_acc.txt 2> $O/shards_acc.err && MSM_ACC_GROUP=0 timeout -k 10 300 python -u tools/shard_study.py --cfgs 20 >> $O/shards_acc.txt 2>> $O/shards_acc.err && MSM_FRONT_GROUP=8 timeout -k 10 300 python -u tools/shard_study.py --cfgs 20,19 >> $O/shards_acc.txt 2>> $O/shards_acc.err; rc=$?; cat $O/shards_acc.txt ;;
+    abitests) timeout -k 10 400 python -u -m pytest tests/test_gpu_blst_ches_abi.py tests/test_gpu_tile_grid.py tests/test_gpu_dropin.py tests/test_gpu_pointer_gather.py tests/test_gpu_parity.py -x -v --timeout 300 --timeout-method thread > $O/pytest_abi.txt 2>&1; rc=$?; tail -3 $O/pytest_abi.txt ;;
+    batchtests) timeout -k 10 500 python -u -m pytest tests/test_gpu_ches.py tests/test_gpu_batch_one_lane.py tests/test_gpu_multi.py -x -v --timeout 300 --timeout-method thread > $O/pytest_batch.txt 2>&1; rc=$?; tail -3 $O/pytest_batch.txt ;;
+    tile) timeout -k 10 300 python -u tools/tile_timing.py > $O/tile.txt 2> $O/tile.err; rc=$?; cat $O/tile.txt; grep "\[tile\]" $O/tile.err ;;
     g2) timeout -k 10 400 python -u bench.py --group 2 --no-configs --no-cpu-baseline > $O/bench_g2.json 2> $O/bench_g2.err; rc=$?
         python3 tools/bench_summary.py $O/bench_g2.json ;;
     prof) cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/bench.py --no-configs --no-cpu-baseline > $O/prof.json 2> $O/prof.log; rc=$?; cd $R ;;
