@@ -1152,7 +1152,16 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
     return e ? (atoi(e) != 0 ? 1 : 0) : -1;
   }();
   const bool l0_first = l0_env < 0 ? G == 1 : l0_env == 1;
-  for (size_t g = 0; g + 1 < (size_t)nfr; ++g) front_group(g);
+  // Fronts run up to nfr - 1 groups ahead on their own stream, but each is
+  // ENQUEUED after the accumulation before it: enqueuing the first nfr - 1
+  // fronts (7 launches each) before the first accumulation cost ~0.3 ms of host
+  // time at the start of a small-MSM batch (profiles/r05_small_trace.txt).
+  // Front g + 1 is always enqueued before accumulation g + 1 waits on it.
+  size_t fronts_issued = 0;
+  auto issue_fronts = [&](size_t upto) {  // every front group <= upto not yet enqueued
+    for (; fronts_issued <= upto && fronts_issued < nfg; ++fronts_issued) front_group(fronts_issued);
+  };
+  issue_fronts(0);
   // Two accumulation lanes (small MSMs, batch_lanes()): MSM k accumulates into
   // bucket set k % 2 on lane stream k % 2 (the caller's s, tails_[0]) and its
   // level 0 follows on the same stream, so accumulations k and k + 1 run side
@@ -1176,7 +1185,6 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
     hipStream_t lane[2] = {s, tails_[0]}, ts = tails_[1];
     for (size_t g = 0; g < nfg; ++g) {
       copy_group(g + nsg);
-      front_group(g + nfr - 1);
       const size_t k0 = fgb[g], k1 = fgb[g + 1];
       const int gb = (int)(g & 1);
       hipStream_t L = lane[gb];
@@ -1205,13 +1213,13 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
         red.copy_out_group(ts, (int)(q % nred), (int)(k - first + 1), (uint8_t *)host_out_ + first * ob);
         MSM_HIP_CHECK(hipEventRecord(evt[q], ts));
       }
+      issue_fronts(g + nfr - 1);
     }
   }
   if (nl >= 2 && !acc_groups) {
     hipStream_t lane[3] = {s, tails_[0], tails_[1]}, ts = nl == 3 ? fstream_ : tails_[1];
     for (size_t g = 0; g < nfg; ++g) {
       copy_group(g + nsg);
-      front_group(g + nfr - 1);
       for (size_t k = fgb[g]; k < fgb[g + 1]; ++k) {
         hipStream_t L = lane[k % nl];
         const size_t q = k / R;
@@ -1235,6 +1243,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
           MSM_HIP_CHECK(hipEventRecord(evt[q], ts));
         }
       }
+      issue_fronts(g + nfr - 1);
     }
   }
   // Level 0 inside the next accumulation's grid (A/B knob, off by default:
@@ -1264,7 +1273,6 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
   };
   for (size_t g = 0; g < (nl >= 2 || !fuse ? 0 : nfg); ++g) {
     copy_group(g + nsg);
-    front_group(g + nfr - 1);
     MSM_HIP_CHECK(hipStreamWaitEvent(s, evf[g], 0));
     for (size_t k = fgb[g]; k < fgb[g + 1]; ++k) {
       const int bset = (int)(k % kBSets);
@@ -1285,6 +1293,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
         l0_group_tail(k - 1);
       }
     }
+    issue_fronts(g + nfr - 1);
   }
   if (fuse && nl < 2) {  // level 0 of the last MSM, alone
     const size_t p = count - 1;
@@ -1295,7 +1304,6 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
   }
   for (size_t g = 0; g < (nl >= 2 || fuse ? 0 : nfg); ++g) {
     copy_group(g + nsg);
-    front_group(g + nfr - 1);  // may start as soon as group g - 1's accumulations release its front set
     MSM_HIP_CHECK(hipStreamWaitEvent(s, evf[g], 0));
     for (size_t k = fgb[g]; k < fgb[g + 1]; ++k) {
       const int bset = (int)(k % kBSets), slot = (int)(k % R), gset = (int)((k / R) % 2);
@@ -1317,6 +1325,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
         red.copy_out_group(ts, gset, slot + 1, (uint8_t *)host_out_ + (k - slot) * ob);
       }
     }
+    issue_fronts(g + nfr - 1);
   }
   // the caller's stream observes completion of every reduction (and front)
   MSM_HIP_CHECK(hipEventRecord(ev_tail_[0], fstream_));

@@ -105,7 +105,7 @@ template <int G>
 Pippenger<G>::~Pippenger() {
   for (auto &e : ev_) (void)hipEventDestroy(e);
   for (auto &e : bev_) (void)hipEventDestroy(e);
-  for (hipStream_t q : {fstream_, lane1_, lane2_, tstream_})
+  for (hipStream_t q : {fstream_, lane1_, tstream_})
     if (q) {
       (void)hipStreamSynchronize(q);
       (void)hipStreamDestroy(q);
@@ -122,7 +122,7 @@ Pippenger<G>::~Pippenger() {
 template <int G>
 size_t Pippenger<G>::device_bytes() const {
   size_t b = stage_ ? stage_->pinned_bytes() : 0;
-  for (const DevBuf *d : {&pts_, &buckets_[0], &buckets_[1], &buckets_[2], &tmp_, &scal_}) b += d->bytes;
+  for (const DevBuf *d : {&pts_, &buckets_[0], &buckets_[1], &gbuckets_[0], &gbuckets_[1], &tmp_, &scal_}) b += d->bytes;
   for (const ChesFrontSet &f : fs_) b += f.device_bytes();
   return b + red_.device_bytes() + (batch_red_ != &red_ ? bred_.device_bytes() : 0);
 }
@@ -152,8 +152,9 @@ void Pippenger<G>::set_points(const void *pts, size_t n, bool on_device, hipStre
 
 template <int C>
 static void launch_digits(hipStream_t s, const uint8_t *sc, size_t stride, size_t n, int nbits, int W, uint32_t *keys,
-                          uint32_t *vals, const uint8_t *neg, int tcl) {
-  hipLaunchKernelGGL(k_digits<C>, dim3(nblk(n, 256)), dim3(256), 0, s, sc, stride, n, nbits, W, keys, vals, neg, tcl);
+                          uint32_t *vals, const uint8_t *neg, int tcl, int nsets, size_t set_stride) {
+  hipLaunchKernelGGL(k_digits<C>, dim3(nblk(n, 256), nsets), dim3(256), 0, s, sc, stride, n, nbits, W, keys, vals, neg,
+                     tcl, set_stride);
 }
 
 #define MSM_C_DISPATCH(c, FN, ...)                          \
@@ -172,26 +173,26 @@ static void launch_digits(hipStream_t s, const uint8_t *sc, size_t stride, size_
 
 template <int G>
 void Pippenger<G>::front(hipStream_t s, const uint8_t *d_scalars, size_t stride, int nbits, const uint8_t *neg,
-                         ChesFrontSet &f) {
+                         ChesFrontSet &f, int nsets, size_t set_stride) {
   const int c = c_;
   const int W = (nbits + 1 + c - 1) / c;
   const size_t NB = (size_t)1 << (c - 1);
   const size_t NT = (size_t)W * NB;
   const size_t n = n_, ne = (size_t)W * n;
-  f.keys.ensure(ne * 4);
-  f.vals.ensure(ne * 4);
-  f.sorted.ensure(ne * 4 + 64);  // + the accumulation's 16-B payload window past a run's end
-  f.counts.ensure(NT * 4);
-  f.offsets.ensure(NT * 4);
-  f.order.ensure(NT * 4);
+  f.keys.ensure(ne * nsets * 4);
+  f.vals.ensure(ne * nsets * 4);
+  f.sorted.ensure(ne * nsets * 4 + 64);  // + the accumulation's 16-B payload window past a run's end
+  f.counts.ensure(NT * nsets * 4);
+  f.offsets.ensure(NT * nsets * 4);
+  f.order.ensure(NT * nsets * 4);
   const bool prof = profile_ && &f == &fs_[0];
   if (prof) MSM_HIP_CHECK(hipEventRecord(ev_[0], s));
   MSM_C_DISPATCH(c, launch_digits, s, d_scalars, stride, n, nbits, W, f.keys.as<uint32_t>(), f.vals.as<uint32_t>(), neg,
-                 top_copies_log2(nbits));
+                 top_copies_log2(nbits), nsets, set_stride);
   MSM_HIP_CHECK(hipGetLastError());
   if (prof) MSM_HIP_CHECK(hipEventRecord(ev_[1], s));
   f.sort.run(s, f.keys.as<uint32_t>(), f.vals.as<uint32_t>(), ne, (uint32_t)NT, f.sorted.as<uint32_t>(),
-             f.counts.as<uint32_t>(), f.offsets.as<uint32_t>(), f.order.as<uint32_t>());
+             f.counts.as<uint32_t>(), f.offsets.as<uint32_t>(), f.order.as<uint32_t>(), nsets);
   if (prof) MSM_HIP_CHECK(hipEventRecord(ev_[2], s));
 }
 
@@ -203,6 +204,16 @@ void Pippenger<G>::accumulate(hipStream_t s, int nbits, ChesFrontSet &f, DevBuf 
   bk.ensure(NT * sizeof(Xyzz<F>));
   launch_accumulate<G>(s, f.sort.sched(f.order.as<uint32_t>(), f.sorted.as<uint32_t>(), 0, NT), pts_.as<Aff<F>>(),
                        bk.as<Xyzz<F>>(), NT);
+  MSM_HIP_CHECK(hipGetLastError());
+}
+
+template <int G>
+void Pippenger<G>::accumulate_sets(hipStream_t s, int nbits, ChesFrontSet &f, int R, DevBuf &bk) {
+  typedef typename FieldOf<G>::F F;
+  const int W = (nbits + 1 + c_ - 1) / c_;
+  const size_t NT = (size_t)W << (c_ - 1);
+  launch_accumulate_sets<G>(s, f.sort.sched(f.order.as<uint32_t>(), f.sorted.as<uint32_t>(), 0, NT), f.sort.stride(NT),
+                            pts_.as<Aff<F>>(), bk.as<Xyzz<F>>(), NT, R);
   MSM_HIP_CHECK(hipGetLastError());
 }
 
@@ -224,9 +235,12 @@ void Pippenger<G>::plan_reduction(int nbits) {
     win[k] = (uint32_t)w;
   }
   red_.plan(wt, win, W);
-  static const int bc_env = [] {  // A/B knob: the batch reducer's level-0 chunk (0: red_'s)
+  // A/B knob: the batch reducer's level-0 chunk; 0 (default): red_'s own
+  // (chunks of 2 at 2^16) -- with front groups of 4, 0.360 vs 0.385 ms per 2^16
+  // MSM for chunks of 8 (profiles/r05_shard_pip_study.txt)
+  static const int bc_env = [] {
     const char *e = getenv("MSM_PIP_L0_CHUNK");
-    return e ? std::max(0, std::min(64, atoi(e))) : 8;
+    return e ? std::max(0, std::min(64, atoi(e))) : 0;
   }();
   if (bc_env && red_.level0_chunk() != bc_env) {
     bred_.plan(wt, win, W, bc_env);
@@ -299,17 +313,8 @@ void Pippenger<G>::run_batch(hipStream_t s, const uint8_t *d_scalars, size_t str
     MSM_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
     MSM_HIP_CHECK(hipStreamCreateWithPriority(&fstream_, hipStreamNonBlocking, greatest));
     MSM_HIP_CHECK(hipStreamCreateWithFlags(&lane1_, hipStreamNonBlocking));
-    MSM_HIP_CHECK(hipStreamCreateWithFlags(&lane2_, hipStreamNonBlocking));
     MSM_HIP_CHECK(hipStreamCreateWithFlags(&tstream_, hipStreamNonBlocking));
   }
-  // accumulation lanes: MSM k accumulates on lane k % nl into bucket set k % nl
-  // and runs its level 0 there; 2 (default) or 3 (MSM_PIP_LANES).  With three
-  // lanes the group tails move to the front stream (the process has 4 hardware
-  // queues, GPU_MAX_HW_QUEUES: one stream per queue).
-  static const int nl = [] {
-    const char *e = getenv("MSM_PIP_LANES");
-    return e ? std::max(1, std::min(3, atoi(e))) : 2;
-  }();
   // the dense stage of the batch's last group over 4 waves per add (nothing left
   // to overlap it with; MSM_TAIL_COOP=0: one lane per add)
   static const bool tail_coop = [] {
@@ -321,6 +326,23 @@ void Pippenger<G>::run_batch(hipStream_t s, const uint8_t *d_scalars, size_t str
     const char *e = getenv("MSM_PIP_GROUP");
     return (size_t)(e ? std::max(1, std::min(32, atoi(e))) : kGroup);
   }();
+  // Front groups: the digits + sort of up to fg_max sets in ONE pass per stage
+  // (7 launches per group instead of per MSM), the group's accumulations in ONE
+  // launch (k_accumulate_sets) and its level 0s in one launch per reduction
+  // group.  A 2^16 MSM's front (digits + two-level sort of 1.25 M entries) took
+  // as long as its accumulation beside the other lane's work, so one front per
+  // MSM on the front stream set the period (profiles/r05_small_trace.txt).
+  // Groups ramp 1, 1, 2, 4, ... so the first accumulation starts after one
+  // front.  MSM_PIP_FRONT_GROUP=<1..8> (1: one MSM per launch, round 4's schedule).
+  static const size_t fg_env = [] {
+    const char *e = getenv("MSM_PIP_FRONT_GROUP");
+    return (size_t)(e ? std::max(1, std::min(8, atoi(e))) : 4);
+  }();
+  const size_t fg_max = fg_env;
+  std::vector<size_t> fgb{0};
+  while (fgb.back() < count)
+    fgb.push_back(std::min(count, fgb.back() + std::min<size_t>(fg_max, std::max<size_t>(1, fgb.back()))));
+  const size_t nfg = fgb.size() - 1;
   const size_t ngroups = (count + group_max - 1) / group_max, R = (count + ngroups - 1) / ngroups;
   const size_t ob = red.out_bytes();
   if (host_out_bytes_ < count * ob) {
@@ -332,46 +354,69 @@ void Pippenger<G>::run_batch(hipStream_t s, const uint8_t *d_scalars, size_t str
     host_out_bytes_ = bytes;
   }
   // every buffer the pipeline touches exists before its first launch (an
-  // allocation inside the issue loop would synchronise the device)
-  for (int b = 0; b < nl; ++b) buckets_[b].ensure(NT * sizeof(Xyzz<F>));
+  // allocation inside the issue loop would synchronise the device): bucket
+  // sets for a whole front group on each lane, reducer sets, and every front
+  // set sized for a whole group (sized by one untimed front of fg_max copies of
+  // set 0, outside the pipeline)
+  for (DevBuf &b : gbuckets_) b.ensure(fg_max * NT * sizeof(Xyzz<F>));
   for (int t = 0; t < kRedSets; ++t) red.ensure_group(t, (int)group_max);
   for (int f = 0; f < kFronts; ++f)
-    if (fs_[f].sorted.bytes < (size_t)W * n_ * 4 + 64) front(s, d_scalars, stride, nbits, nullptr, fs_[f]);
+    if (fs_[f].sorted.bytes < (size_t)W * n_ * fg_max * 4 + 64)
+      front(s, d_scalars, stride, nbits, nullptr, fs_[f], (int)fg_max, 0);
   MSM_HIP_CHECK(hipStreamSynchronize(s));
-  while (bev_.size() < 3 * count + ngroups + 1) {
+  while (bev_.size() < 2 * count + nfg + ngroups + 1) {
     hipEvent_t e;
     MSM_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     bev_.push_back(e);
   }
-  hipEvent_t *evf = bev_.data() + 1, *eva = evf + count, *evh = eva + count, *evt = evh + count;
+  hipEvent_t *eva = bev_.data() + 1, *evh = eva + count, *evf = evh + count, *evt = evf + nfg;
   MSM_HIP_CHECK(hipEventRecord(bev_[0], s));
-  for (hipStream_t q : {fstream_, lane1_, lane2_, tstream_}) MSM_HIP_CHECK(hipStreamWaitEvent(q, bev_[0], 0));
-  auto front_k = [&](size_t k) {
-    if (k >= count) return;
-    if (k >= (size_t)kFronts) MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, eva[k - kFronts], 0));  // front set free
-    front(fstream_, d_scalars + k * set_stride, stride, nbits, nullptr, fs_[k % kFronts]);
-    MSM_HIP_CHECK(hipEventRecord(evf[k], fstream_));
+  for (hipStream_t q : {fstream_, lane1_, tstream_}) MSM_HIP_CHECK(hipStreamWaitEvent(q, bev_[0], 0));
+  auto front_group = [&](size_t g) {
+    if (g >= nfg) return;
+    if (g >= (size_t)kFronts)  // front set g % kFronts: group g - kFronts's accumulation has read it
+      MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, eva[fgb[g - kFronts + 1] - 1], 0));
+    front(fstream_, d_scalars + fgb[g] * set_stride, stride, nbits, nullptr, fs_[g % kFronts],
+          (int)(fgb[g + 1] - fgb[g]), set_stride);
+    MSM_HIP_CHECK(hipEventRecord(evf[g], fstream_));
   };
-  hipStream_t lane[3] = {s, lane1_, lane2_}, ts = nl == 3 ? fstream_ : tstream_;
-  for (size_t k = 0; k + 1 < (size_t)kFronts; ++k) front_k(k);
-  for (size_t k = 0; k < count; ++k) {
-    front_k(k + kFronts - 1);
-    hipStream_t L = lane[k % nl];
-    const size_t q = k / R;
-    const int slot = (int)(k % R), gset = (int)(q % kRedSets);
-    MSM_HIP_CHECK(hipStreamWaitEvent(L, evf[k], 0));
-    if (q >= (size_t)kRedSets && slot < nl)  // reducer set q % kRedSets free again (tail q - kRedSets)
-      MSM_HIP_CHECK(hipStreamWaitEvent(L, evt[q - kRedSets], 0));
-    accumulate(L, nbits, fs_[k % kFronts], buckets_[k % nl]);  // bucket set k % nl: lane k % nl only, in order
-    MSM_HIP_CHECK(hipEventRecord(eva[k], L));
-    red.launch_head_slot(L, buckets_[k % nl].p, gset, slot);
-    MSM_HIP_CHECK(hipEventRecord(evh[k], L));
-    if ((size_t)slot + 1 == R || k + 1 == count) {
-      for (int d = 0; d < nl && d <= slot; ++d) MSM_HIP_CHECK(hipStreamWaitEvent(ts, evh[k - d], 0));
-      red.launch_tail_group(ts, gset, slot + 1, tail_coop && k + 1 == count);
-      red.copy_out_group(ts, gset, slot + 1, (uint8_t *)host_out_ + (k - slot) * ob);
-      MSM_HIP_CHECK(hipEventRecord(evt[q], ts));
+  // accumulation groups alternate between two lane streams (the caller's and
+  // lane1_); group tails on tstream_
+  hipStream_t lane[2] = {s, lane1_};
+  // fronts run up to kFronts - 1 groups ahead, each ENQUEUED after the
+  // accumulation before it (enqueuing four fronts before the first accumulation
+  // cost ~0.3 ms of host time per batch); front g + 1 is always enqueued before
+  // accumulation g + 1 waits on it
+  size_t fronts_issued = 0;
+  auto issue_fronts = [&](size_t upto) {
+    for (; fronts_issued <= upto && fronts_issued < nfg; ++fronts_issued) front_group(fronts_issued);
+  };
+  issue_fronts(0);
+  for (size_t g = 0; g < nfg; ++g) {
+    const size_t k0 = fgb[g], k1 = fgb[g + 1];
+    const int gb = (int)(g & 1);
+    hipStream_t L = lane[gb];
+    MSM_HIP_CHECK(hipStreamWaitEvent(L, evf[g], 0));
+    accumulate_sets(L, nbits, fs_[g % kFronts], (int)(k1 - k0), gbuckets_[gb]);  // bucket sets: lane gb only, in order
+    for (size_t k = k0; k < k1; ++k) MSM_HIP_CHECK(hipEventRecord(eva[k], L));
+    for (size_t a = k0; a < k1;) {  // level 0, one launch per reduction group touched
+      const size_t q = a / R, b = std::min(k1, (q + 1) * R);
+      if (q >= (size_t)kRedSets) MSM_HIP_CHECK(hipStreamWaitEvent(L, evt[q - kRedSets], 0));  // reducer set free again
+      red.launch_head_slots(L, gbuckets_[gb].as<uint8_t>() + (a - k0) * NT * sizeof(Xyzz<F>), NT,
+                            (int)(q % kRedSets), (int)(a % R), (int)(b - a));
+      a = b;
     }
+    for (size_t k = k0; k < k1; ++k) MSM_HIP_CHECK(hipEventRecord(evh[k], L));
+    for (size_t k = k0; k < k1; ++k) {  // tails of the reduction groups ending in [k0, k1)
+      if ((k + 1) % R != 0 && k + 1 != count) continue;
+      const size_t q = k / R, first = q * R;
+      MSM_HIP_CHECK(hipStreamWaitEvent(tstream_, evh[k], 0));                                     // this lane's level 0s
+      if (k0 >= 1 && k0 - 1 >= first) MSM_HIP_CHECK(hipStreamWaitEvent(tstream_, evh[k0 - 1], 0));  // the other lane's
+      red.launch_tail_group(tstream_, (int)(q % kRedSets), (int)(k - first + 1), tail_coop && k + 1 == count);
+      red.copy_out_group(tstream_, (int)(q % kRedSets), (int)(k - first + 1), (uint8_t *)host_out_ + first * ob);
+      MSM_HIP_CHECK(hipEventRecord(evt[q], tstream_));
+    }
+    issue_fronts(g + kFronts - 1);
   }
   // the host Horner of group q overlaps the GPU work of later groups
   for (size_t q = 0; q * R < count; ++q) {
@@ -380,7 +425,7 @@ void Pippenger<G>::run_batch(hipStream_t s, const uint8_t *d_scalars, size_t str
       outs[k] = red.combine_windows((const uint8_t *)host_out_ + k * ob, c_);
   }
   // the caller's stream observes completion of every stream of the batch
-  for (hipStream_t q : {fstream_, lane1_, lane2_, tstream_}) {
+  for (hipStream_t q : {fstream_, lane1_, tstream_}) {
     MSM_HIP_CHECK(hipEventRecord(bev_[0], q));
     MSM_HIP_CHECK(hipStreamWaitEvent(s, bev_[0], 0));
   }

@@ -315,26 +315,30 @@ class Pippenger {
   PhaseTimes times_;
   static constexpr int kFronts = 5, kGroup = 8, kRedSets = 4;
   ChesFrontSet fs_[kFronts];  // digit/sort outputs: fs_[0] for run(), all of them for run_batch()
-  DevBuf pts_, buckets_[3], tmp_, scal_;  // buckets: one set per batch lane
+  DevBuf pts_, buckets_[2], tmp_, scal_;
   std::unique_ptr<HostStager> stage_;  // run_host: uploads from the caller's pageable memory
   hipStream_t up_ = nullptr;  // run_host: point upload stream
   hipEvent_t ev_up_ = nullptr, ev_s_ = nullptr;
   // run_batch: front stream, second accumulation lane, tail stream; events; read-back slots
-  // run_batch streams: fronts, lanes 1 and 2 (lane 0 is the caller's), tails
-  hipStream_t fstream_ = nullptr, lane1_ = nullptr, lane2_ = nullptr, tstream_ = nullptr;
+  // run_batch streams: fronts, lane 1 (lane 0 is the caller's), tails
+  hipStream_t fstream_ = nullptr, lane1_ = nullptr, tstream_ = nullptr;
   std::vector<hipEvent_t> bev_;
   void *host_out_ = nullptr;
   size_t host_out_bytes_ = 0;
   // digits + sort into f; neg: optional per-point sign flips (tiles)
-  void front(hipStream_t s, const uint8_t *d_scalars, size_t stride, int nbits, const uint8_t *neg, ChesFrontSet &f);
+  // nsets > 1: a front group of nsets scalar sets set_stride bytes apart in one pass
+  void front(hipStream_t s, const uint8_t *d_scalars, size_t stride, int nbits, const uint8_t *neg, ChesFrontSet &f,
+             int nsets = 1, size_t set_stride = 0);
   void accumulate(hipStream_t s, int nbits, ChesFrontSet &f, DevBuf &buckets);
+  // the R sets of a front group in one launch, set r's buckets at r NT in bk
+  void accumulate_sets(hipStream_t s, int nbits, ChesFrontSet &f, int R, DevBuf &bk);
+  DevBuf gbuckets_[2];  // run_batch accumulation groups: two lanes x front-group bucket sets
   void plan_reduction(int nbits);  // reducer plan for this window layout (built once)
   void back(hipStream_t s, int nbits, hfp::Jac<HF> *out);  // accumulate + reduce + read-back (fs_[0])
   WeightedReducer<G> red_;
-  // run_batch's reducer: the same weights with level-0 chunks of 8 when red_
-  // (planned for the synchronous MSM's latency) chunks by less -- in a batch
-  // level 0 runs beside the other lane's accumulation, the grouped tail beside
-  // later MSMs (MSM_PIP_L0_CHUNK=<2..64> overrides, 0 reuses red_)
+  // run_batch's reducer: red_, or with MSM_PIP_L0_CHUNK=<2..64> the same
+  // weights planned with that level-0 chunk (chunks of 8 measured slower than
+  // red_'s 2 at 2^16)
   WeightedReducer<G> bred_;
   WeightedReducer<G> *batch_red_ = &red_;
   int red_W_ = 0, red_tcl_ = -1;  // window count / top copies the reducer plan was built for

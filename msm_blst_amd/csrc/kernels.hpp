@@ -170,15 +170,19 @@ __device__ __forceinline__ uint32_t scalar_bits(const uint32_t s[10], int off, i
 // n / 2^topbits sequential madds there.  Its NB slots instead hold 2^tcl copies
 // of its 2^topbits buckets (entry i -> copy i mod 2^tcl), each copy weighted
 // like its bucket in the reduction plan (Pippenger<G>::back).
+// blockIdx.y = scalar set r of a front group (scalars + r set_stride; entries
+// at keys / vals + r W n)
 template <int C>
 __global__ void k_digits(const uint8_t *__restrict__ scalars, size_t stride, size_t n, int nbits, int W,
                          uint32_t *__restrict__ keys, uint32_t *__restrict__ vals, const uint8_t *__restrict__ neg,
-                         int tcl) {
+                         int tcl, size_t set_stride) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t flip = neg ? (uint32_t)(neg[i] != 0) : 0u;
   constexpr uint32_t NB = 1u << (C - 1);
-  const uint8_t *sp = scalars + i * stride;
+  const uint8_t *sp = scalars + blockIdx.y * set_stride + i * stride;
+  keys += (size_t)blockIdx.y * W * n;
+  vals += (size_t)blockIdx.y * W * n;
   int nbytes = (nbits + 7) / 8;
   uint32_t s[10];
 #pragma unroll

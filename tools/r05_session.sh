@@ -18,8 +18,11 @@ for step in "$@"; do
     bench) timeout -k 10 600 python -u bench.py > $O/bench.json 2> $O/bench.err; rc=$?
            python3 tools/bench_summary.py $O/bench.json ;;
     shards) timeout -k 10 400 python -u tools/shard_study.py > $O/shards.txt 2> $O/shards.err; rc=$?; cat $O/shards.txt ;;
-    pip) timeout -k 10 500 python -u tools/pip_study.py --envs "MSM_PIP_L0_CHUNK=0 MSM_TAIL_COOP=0;MSM_PIP_L0_CHUNK=0;MSM_PIP_L0_CHUNK=8;MSM_PIP_L0_CHUNK=8 MSM_PIP_LANES=3;MSM_PIP_L0_CHUNK=4 MSM_PIP_LANES=3" > $O/pip.txt 2> $O/pip.err; rc=$?; cat $O/pip.txt ;;
+    pip) timeout -k 10 500 python -u tools/pip_study.py --windows 13,14,15 --envs "MSM_PIP_FRONT_GROUP=1;MSM_PIP_FRONT_GROUP=2;MSM_PIP_FRONT_GROUP=4;MSM_PIP_FRONT_GROUP=8;MSM_PIP_FRONT_GROUP=4 MSM_PIP_L0_CHUNK=0" > $O/pip.txt 2> $O/pip.err; rc=$?; cat $O/pip.txt ;;
+    piptests) timeout -k 10 300 python -u -m pytest tests/test_gpu_pippenger_batch.py tests/test_gpu_parity.py -x -v --timeout 300 --timeout-method thread > $O/pytest_pip.txt 2>&1; rc=$?; tail -3 $O/pytest_pip.txt ;;
     shards_ab) timeout -k 10 500 python -u tools/shard_study.py --cfgs 20,19 > $O/shards_ab.txt 2> $O/shards_ab.err && MSM_BATCH_L0_CHUNK=0 MSM_TAIL_COOP=0 timeout -k 10 500 python -u tools/shard_study.py --cfgs 20,19 >> $O/shards_ab.txt 2>> $O/shards_ab.err; rc=$?; cat $O/shards_ab.txt ;;
+    ptrace) cd /tmp && MSM_PIP_L0_CHUNK=0 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/ptrace -o run -- python3 $R/tools/r04_small_trace.py pb16 > $O/ptrace.txt 2> $O/ptrace.err; rc=$?; cd $R
+           cat $O/ptrace.txt; python3 tools/batch_profile.py $O/ptrace/run_kernel_trace.csv > $O/ptrace_profile.txt; cat $O/ptrace_profile.txt ;;
     trace) cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/trace -o run -- python3 $R/tools/r04_small_trace.py pb16 c17 > $O/trace.txt 2> $O/trace.err; rc=$?; cd $R
            cat $O/trace.txt; python3 tools/batch_profile.py $O/trace/run_kernel_trace.csv > $O/trace_profile.txt; cat $O/trace_profile.txt ;;
     shards_acc) timeout -k 10 300 python -u tools/shard_study.py --cfgs 20,19 > $O/shards_acc.txt 2> $O/shards_acc.err && MSM_ACC_GROUP=0 timeout -k 10 300 python -u tools/shard_study.py --cfgs 20 >> $O/shards_acc.txt 2>> $O/shards_acc.err && MSM_FRONT_GROUP=8 timeout -k 10 300 python -u tools/shard_study.py --cfgs 20,19 >> $O/shards_acc.txt 2>> $O/shards_acc.err; rc=$?; cat $O/shards_acc.txt ;;
