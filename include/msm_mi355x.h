@@ -301,6 +301,11 @@ size_t msm_ches_ctx_bucket_count(const msm_ches_ctx *ctx);
  * one accumulation fills the chip >= 3 wave-slot rounds deep, else 2-3 MSMs
  * accumulate side by side (MSM_BATCH_LANES overrides); 0 on a NULL ctx */
 int msm_ches_ctx_batch_lanes(const msm_ches_ctx *ctx);
+/* diagnostic (single-device contexts): digits + sort of nsets scalar sets in
+ * DEVICE memory (set_stride bytes apart, 32-byte scalars), then the mean ms of
+ * reps launches accumulating all nsets sets in one grid, alone on the stream */
+int msm_ches_ctx_time_accumulation(msm_ches_ctx *ctx, const byte *scalars_dev, size_t set_stride, int nsets, int reps,
+                                   float *ms_per_launch);
 void msm_ches_ctx_destroy(msm_ches_ctx *ctx);
 
 /* ---- BGMW95 fixed-base method, device-resident precomputed table ----

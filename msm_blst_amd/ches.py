@@ -135,6 +135,13 @@ class CHESContext:
         """Accumulation lanes mult_batch runs (1: the one-lane schedule of the 2^20 headline)."""
         return lib().msm_ches_ctx_batch_lanes(self._ctx)
 
+    def time_accumulation(self, scalars_dev, nsets, reps=5, set_stride=None):
+        """Diagnostic: ms of one launch accumulating nsets device scalar sets (after their front)."""
+        ms = ctypes.c_float()
+        check(lib().msm_ches_ctx_time_accumulation(self._ctx, scalars_dev, set_stride or self.n * 32, nsets, reps,
+                                                   ctypes.byref(ms)))
+        return ms.value
+
     def set_profiling(self, on=True):
         check(lib().msm_ches_ctx_set_profiling(self._ctx, int(on)))
 

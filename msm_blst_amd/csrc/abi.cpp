@@ -970,6 +970,20 @@ size_t msm_ches_ctx_bucket_count(const msm_ches_ctx *ctx) { return ctx ? CHES_DI
 
 int msm_ches_ctx_batch_lanes(const msm_ches_ctx *ctx) { return ctx ? CHES_DISPATCH(ctx, front().batch_lanes()) : 0; }
 
+int msm_ches_ctx_time_accumulation(msm_ches_ctx *ctx, const byte *scalars, size_t set_stride, int nsets, int reps,
+                                   float *ms) {
+  if (!ctx || !scalars || !ms || nsets < 1 || reps < 1) return fail(MSM_E_ARG, "bad args");
+  if (!ctx->ready) return fail(MSM_E_STATE, "no table");
+  if ((ctx->group == 1 ? ctx->g1->engines() : ctx->g2->engines()) != 1) return fail(MSM_E_ARG, "single-device contexts only");
+  try {
+    DeviceGuard g(ctx->device);
+    *ms = CHES_DISPATCH(ctx, front().time_accumulation((hipStream_t)0, scalars, set_stride, nsets, reps));
+    return MSM_OK;
+  } catch (const std::exception &e) {
+    return fail(MSM_E_HIP, e.what());
+  }
+}
+
 void msm_ches_ctx_destroy(msm_ches_ctx *ctx) { delete ctx; }
 
 // ---------------- BGMW95 contexts ----------------

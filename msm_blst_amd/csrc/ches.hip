@@ -833,6 +833,27 @@ void Ches<G>::accumulate_sets(hipStream_t s, int set, int R, int gb, const void 
 }
 
 template <int G>
+float Ches<G>::time_accumulation(hipStream_t s, const uint8_t *d_scalars, size_t set_stride, int nsets, int reps) {
+  DeviceGuard g(dev_);
+  if (n_ == 0 || nsets < 1 || reps < 1) throw std::runtime_error("time_accumulation: no table / bad arguments");
+  digits_sort(s, d_scalars, 32, set_stride, nsets, 0);
+  gbuckets_[0].ensure((size_t)nsets * bucket_count() * sizeof(Xyzz<typename FieldOf<G>::F>));
+  accumulate_sets(s, 0, nsets, 0, nullptr);  // warm
+  hipEvent_t a, b;
+  MSM_HIP_CHECK(hipEventCreate(&a));
+  MSM_HIP_CHECK(hipEventCreate(&b));
+  MSM_HIP_CHECK(hipEventRecord(a, s));
+  for (int r = 0; r < reps; ++r) accumulate_sets(s, 0, nsets, 0, nullptr);
+  MSM_HIP_CHECK(hipEventRecord(b, s));
+  MSM_HIP_CHECK(hipEventSynchronize(b));
+  float ms = 0;
+  MSM_HIP_CHECK(hipEventElapsedTime(&ms, a, b));
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  return ms / (float)reps;
+}
+
+template <int G>
 void Ches<G>::accumulate_l0(hipStream_t s, int set, int r, int bset, const void *table, int l0_bset, int gset,
                             int slot, int l0_last) {
   typedef typename FieldOf<G>::F F;
@@ -986,7 +1007,13 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
     return !e || atoi(e) != 0;
   }();
   const bool acc_groups = nl >= 2 && nseg == 1 && acc_group_env;
+  // one lane (the 2^20 headline): accumulation groups of kFrontGroupDefault
+  // sets per launch (one launch's last waves run with the chip half idle: alone,
+  // 1.96 ms for one 2^20 set vs 1.70 per set for two in one grid,
+  // profiles/r05_acc_rate.txt); MSM_ACC_GROUP=0 or MSM_FRONT_GROUP=1: one
+  // accumulation per MSM
   const size_t fg_max = !packed ? 1 : fg_env ? fg_env : acc_groups ? 4 : nl >= 3 ? 4 : nl == 2 ? 2 : (size_t)kFrontGroupDefault;
+  const bool acc_groups1 = nl < 2 && nseg == 1 && acc_group_env && fg_max > 1;
   // front groups of 1, 1, 2, 4, then fg_max MSMs: the first accumulation
   // starts after one front, and each group's host sets (copied while the earlier
   // groups accumulate: a set copies in ~0.6 ms, an MSM accumulates in ~2.3) are
@@ -999,7 +1026,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
   // every buffer the loop touches exists before the first launch (an allocation
   // inside the issue loop could synchronise the device)
   const size_t NB = bucket_count(), n = n_;
-  if (acc_groups)
+  if (acc_groups || acc_groups1)
     for (DevBuf &b : gbuckets_) b.ensure(fg_max * NB * sizeof(Xyzz<typename FieldOf<G>::F>));
   else
     for (int b = 0; b < std::max(kBSets, nl); ++b) buckets_[b].ensure(NB * sizeof(Xyzz<typename FieldOf<G>::F>));
@@ -1012,7 +1039,26 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
   // reuse reducer set q % 4 after tail q - 4 (a tail is ~30 latency-bound
   // launches, ~1 ms beside the accumulations: with 2 sets group q + 2 waited
   // for it, profiles/r04_batch_trace_2p17.txt)
-  const int nfr = nl >= 2 ? kFrontsMax : kFronts, nred = nl >= 2 ? 4 : 2;
+  // Front phase (small-MSM accumulation groups; MSM_FRONT_PHASE=1 enables):
+  // one front set per front group, up to kFrontPhase (capped at ~4 GiB of
+  // front sets), and the first accumulation waits for every front of that
+  // phase.  Fronts beside accumulations starve (their 1024-thread fine-pass
+  // workgroups wait for a whole CU to drain: 1.1-1.6 ms instead of 34 us in the
+  // 2^17 trace, profiles/r05_small_trace.txt); run first, on the whole chip,
+  // the batch's fronts take ~60 us per set and the accumulations then run
+  // without them.
+  // measured slower, so off by default: 2^17 shard 0.461 vs 0.438 ms per MSM,
+  // 2^16 plain 0.385 vs 0.368 (profiles/r05_shard_pip_study.txt)
+  static const bool phase_env = [] {
+    const char *e = getenv("MSM_FRONT_PHASE");
+    return e && atoi(e) != 0;
+  }();
+  const bool phase = acc_groups && phase_env;
+  const size_t fs_bytes = fg_max * n * (size_t)p_.h * 16 + 1;  // ~ one front set (sorted, ranks, interleave)
+  const int nfr = phase ? (int)std::max<size_t>(kFrontsMax, std::min<size_t>(kFrontPhase, ((size_t)4 << 30) / fs_bytes))
+                        : nl >= 2 ? kFrontsMax : kFronts;
+  const int nred = nl >= 2 ? 4 : 2;
+  if ((int)fs_.size() < nfr) fs_.resize(nfr);
   for (int t = 0; t < nred; ++t) red.ensure_group(t, (int)group_max);
   // front sets sized for a whole front group (the sort's scan scratch too): run
   // one sort of fg_max sets per set before the loop if they are not yet sized
@@ -1161,7 +1207,8 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
   auto issue_fronts = [&](size_t upto) {  // every front group <= upto not yet enqueued
     for (; fronts_issued <= upto && fronts_issued < nfg; ++fronts_issued) front_group(fronts_issued);
   };
-  issue_fronts(0);
+  const size_t nphase = phase ? std::min(nfg, (size_t)nfr) : 1;  // fronts before the first accumulation
+  issue_fronts(nphase - 1);
   // Two accumulation lanes (small MSMs, batch_lanes()): MSM k accumulates into
   // bucket set k % 2 on lane stream k % 2 (the caller's s, tails_[0]) and its
   // level 0 follows on the same stream, so accumulations k and k + 1 run side
@@ -1189,6 +1236,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
       const int gb = (int)(g & 1);
       hipStream_t L = lane[gb];
       MSM_HIP_CHECK(hipStreamWaitEvent(L, evf[g], 0));
+      if (g == 0 && nphase > 1) MSM_HIP_CHECK(hipStreamWaitEvent(L, evf[nphase - 1], 0));  // the front phase
       if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k0], L));
       accumulate_sets(L, (int)(g % nfr), (int)(k1 - k0), gb, job_table(k0));
       if (prof) {
@@ -1302,7 +1350,46 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
     MSM_HIP_CHECK(hipEventRecord(evh[p], s));
     l0_group_tail(p);
   }
-  for (size_t g = 0; g < (nl >= 2 || fuse ? 0 : nfg); ++g) {
+  // One lane, accumulation groups: front group g's sets accumulate in ONE launch
+  // on the caller's stream into gbuckets_[g % 2] (after group g - 2's level 0s
+  // released it, and -- the level-0 wait -- after group g - 1's); each part of
+  // the group in reduction group q runs its level 0s in one launch on tails_[q % 2],
+  // followed there by q's tail when q ends inside the group.
+  for (size_t g = 0; g < (acc_groups1 && !fuse ? nfg : 0); ++g) {
+    copy_group(g + nsg);
+    const size_t k0 = fgb[g], k1 = fgb[g + 1];
+    const int gb = (int)(g & 1);
+    MSM_HIP_CHECK(hipStreamWaitEvent(s, evf[g], 0));
+    // every level 0 of group g - 2 (gbuckets_[gb] free again) and, the level-0
+    // wait, of group g - 1 (a group straddling two reduction groups ran its
+    // level 0s on both tail streams)
+    if (g >= 2)
+      for (size_t k = fgb[g - 2]; k < fgb[g - 1]; ++k) MSM_HIP_CHECK(hipStreamWaitEvent(s, evh[k], 0));
+    if (l0_first && g >= 1)
+      for (size_t k = fgb[g - 1]; k < k0; ++k) MSM_HIP_CHECK(hipStreamWaitEvent(s, evh[k], 0));
+    if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k0], s));
+    accumulate_sets(s, (int)(g % nfr), (int)(k1 - k0), gb, job_table(k0));
+    if (prof) {
+      MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k0 + 1], s));
+      prof_k.push_back(k0);
+    }
+    for (size_t k = k0; k < k1; ++k) MSM_HIP_CHECK(hipEventRecord(eva[k], s));
+    for (size_t a = k0; a < k1;) {
+      const size_t q = a / R, b = std::min(k1, (q + 1) * R);
+      hipStream_t ts = tails_[q % 2];
+      MSM_HIP_CHECK(hipStreamWaitEvent(ts, eva[k1 - 1], 0));
+      red.launch_head_slots(ts, gbuckets_[gb].as<uint8_t>() + (a - k0) * NB * sizeof(Xyzz<typename FieldOf<G>::F>), NB,
+                            (int)(q % 2), (int)(a % R), (int)(b - a));
+      for (size_t k = a; k < b; ++k) MSM_HIP_CHECK(hipEventRecord(evh[k], ts));
+      if (b % R == 0 || b == count) {  // reduction group q ends here
+        red.launch_tail_group(ts, (int)(q % 2), (int)(b - q * R), tail_coop && b == count);
+        red.copy_out_group(ts, (int)(q % 2), (int)(b - q * R), (uint8_t *)host_out_ + q * R * ob);
+      }
+      a = b;
+    }
+    issue_fronts(g + nfr - 1);
+  }
+  for (size_t g = 0; g < (nl >= 2 || fuse || acc_groups1 ? 0 : nfg); ++g) {
     copy_group(g + nsg);
     MSM_HIP_CHECK(hipStreamWaitEvent(s, evf[g], 0));
     for (size_t k = fgb[g]; k < fgb[g + 1]; ++k) {

@@ -358,9 +358,20 @@ void Pippenger<G>::run_batch(hipStream_t s, const uint8_t *d_scalars, size_t str
   // sets for a whole front group on each lane, reducer sets, and every front
   // set sized for a whole group (sized by one untimed front of fg_max copies of
   // set 0, outside the pipeline)
+  // Front phase (MSM_FRONT_PHASE=1; off: measured slower, Ches::run_jobs): one
+  // front set per front group, up to kFrontPhase (~4 GiB of front sets at
+  // most), the first accumulation waiting for every front of the phase
+  static const bool phase_env = [] {
+    const char *e = getenv("MSM_FRONT_PHASE");
+    return e && atoi(e) != 0;
+  }();
+  const size_t fs_bytes = fg_max * (size_t)W * n_ * 24 + 1;  // ~ one front set (keys, vals, sorted, sort scratch)
+  const int nfr = phase_env ? (int)std::max<size_t>(kFronts, std::min<size_t>(kFrontPhase, ((size_t)4 << 30) / fs_bytes))
+                            : kFronts;
+  if ((int)fs_.size() < nfr) fs_.resize(nfr);
   for (DevBuf &b : gbuckets_) b.ensure(fg_max * NT * sizeof(Xyzz<F>));
   for (int t = 0; t < kRedSets; ++t) red.ensure_group(t, (int)group_max);
-  for (int f = 0; f < kFronts; ++f)
+  for (int f = 0; f < nfr; ++f)
     if (fs_[f].sorted.bytes < (size_t)W * n_ * fg_max * 4 + 64)
       front(s, d_scalars, stride, nbits, nullptr, fs_[f], (int)fg_max, 0);
   MSM_HIP_CHECK(hipStreamSynchronize(s));
@@ -374,9 +385,9 @@ void Pippenger<G>::run_batch(hipStream_t s, const uint8_t *d_scalars, size_t str
   for (hipStream_t q : {fstream_, lane1_, tstream_}) MSM_HIP_CHECK(hipStreamWaitEvent(q, bev_[0], 0));
   auto front_group = [&](size_t g) {
     if (g >= nfg) return;
-    if (g >= (size_t)kFronts)  // front set g % kFronts: group g - kFronts's accumulation has read it
-      MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, eva[fgb[g - kFronts + 1] - 1], 0));
-    front(fstream_, d_scalars + fgb[g] * set_stride, stride, nbits, nullptr, fs_[g % kFronts],
+    if (g >= (size_t)nfr)  // front set g % nfr: group g - nfr's accumulation has read it
+      MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, eva[fgb[g - nfr + 1] - 1], 0));
+    front(fstream_, d_scalars + fgb[g] * set_stride, stride, nbits, nullptr, fs_[g % nfr],
           (int)(fgb[g + 1] - fgb[g]), set_stride);
     MSM_HIP_CHECK(hipEventRecord(evf[g], fstream_));
   };
@@ -391,13 +402,15 @@ void Pippenger<G>::run_batch(hipStream_t s, const uint8_t *d_scalars, size_t str
   auto issue_fronts = [&](size_t upto) {
     for (; fronts_issued <= upto && fronts_issued < nfg; ++fronts_issued) front_group(fronts_issued);
   };
-  issue_fronts(0);
+  const size_t nphase = phase_env ? std::min(nfg, (size_t)nfr) : 1;  // fronts before the first accumulation
+  issue_fronts(nphase - 1);
   for (size_t g = 0; g < nfg; ++g) {
     const size_t k0 = fgb[g], k1 = fgb[g + 1];
     const int gb = (int)(g & 1);
     hipStream_t L = lane[gb];
     MSM_HIP_CHECK(hipStreamWaitEvent(L, evf[g], 0));
-    accumulate_sets(L, nbits, fs_[g % kFronts], (int)(k1 - k0), gbuckets_[gb]);  // bucket sets: lane gb only, in order
+    if (g == 0 && nphase > 1) MSM_HIP_CHECK(hipStreamWaitEvent(L, evf[nphase - 1], 0));  // the front phase
+    accumulate_sets(L, nbits, fs_[g % nfr], (int)(k1 - k0), gbuckets_[gb]);  // bucket sets: lane gb only, in order
     for (size_t k = k0; k < k1; ++k) MSM_HIP_CHECK(hipEventRecord(eva[k], L));
     for (size_t a = k0; a < k1;) {  // level 0, one launch per reduction group touched
       const size_t q = a / R, b = std::min(k1, (q + 1) * R);
@@ -416,7 +429,7 @@ void Pippenger<G>::run_batch(hipStream_t s, const uint8_t *d_scalars, size_t str
       red.copy_out_group(tstream_, (int)(q % kRedSets), (int)(k - first + 1), (uint8_t *)host_out_ + first * ob);
       MSM_HIP_CHECK(hipEventRecord(evt[q], tstream_));
     }
-    issue_fronts(g + kFronts - 1);
+    issue_fronts(g + nfr - 1);
   }
   // the host Horner of group q overlaps the GPU work of later groups
   for (size_t q = 0; q * R < count; ++q) {

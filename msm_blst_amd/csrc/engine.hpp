@@ -314,7 +314,10 @@ class Pippenger {
   bool profile_ = false;
   PhaseTimes times_;
   static constexpr int kFronts = 5, kGroup = 8, kRedSets = 4;
-  ChesFrontSet fs_[kFronts];  // digit/sort outputs: fs_[0] for run(), all of them for run_batch()
+  // digit/sort outputs: fs_[0] for run(); run_batch rotates kFronts of them, or
+  // with the front phase one per front group (up to kFrontPhase)
+  std::vector<ChesFrontSet> fs_ = std::vector<ChesFrontSet>(kFronts);
+  static constexpr int kFrontPhase = 16;
   DevBuf pts_, buckets_[2], tmp_, scal_;
   std::unique_ptr<HostStager> stage_;  // run_host: uploads from the caller's pageable memory
   hipStream_t up_ = nullptr;  // run_host: point upload stream
@@ -400,6 +403,10 @@ class Ches {
   const PhaseTimes &times() const { return times_; }
   int device() const { return dev_; }
   int batch_lanes() const;  // accumulation streams of run_batch (1, 2 or 3)
+  // diagnostic: digits + sort of nsets device scalar sets (set_stride apart) in
+  // one front, then the ms of ONE launch accumulating all of them (mean of reps
+  // launches, HIP events on stream s); nothing else runs beside it
+  float time_accumulation(hipStream_t s, const uint8_t *d_scalars, size_t set_stride, int nsets, int reps);
 
  private:
   int dev_;
@@ -433,11 +440,14 @@ class Ches {
   // 8 measured +1.2 % (profiles/r04_red_group_ab.txt).  MSM_RED_GROUP overrides.
   static constexpr int kGroup = 20;
   static constexpr int kFrontGroup = 8;  // batch: largest front group (ramping up 1, 1, 2, 4, 8)
-  static constexpr int kFrontGroupDefault = 1;
+  static constexpr int kFrontGroupDefault = 2;  // one-lane batch: sets per front / accumulation group
   // front k+1 may start when accumulation k-2 ends (slack for the copies); the
   // lane schedule of small MSMs rotates kFrontsMax sets (fronts further ahead)
   static constexpr int kFronts = 3, kFrontsMax = 5;
-  ChesFrontSet fs_[kFrontsMax];
+  // front sets: kFronts / kFrontsMax in rotation, or with the front phase of
+  // the small-MSM batch one per front group (up to kFrontPhase)
+  std::vector<ChesFrontSet> fs_ = std::vector<ChesFrontSet>(kFrontsMax);
+  static constexpr int kFrontPhase = 16;
   // host scalar sets of a batch: two groups of kFrontGroup device slots, copied on
   // their own stream (cstream_) ahead of the group's front
   DevBuf scal_;
