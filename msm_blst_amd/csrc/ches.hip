@@ -1007,13 +1007,13 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
     return !e || atoi(e) != 0;
   }();
   const bool acc_groups = nl >= 2 && nseg == 1 && acc_group_env;
-  // one lane (the 2^20 headline): accumulation groups of kFrontGroupDefault
-  // sets per launch (one launch's last waves run with the chip half idle: alone,
-  // 1.96 ms for one 2^20 set vs 1.70 per set for two in one grid,
-  // profiles/r05_acc_rate.txt); MSM_ACC_GROUP=0 or MSM_FRONT_GROUP=1: one
-  // accumulation per MSM
+  // (one lane, the 2^20 headline: one accumulation launch per MSM.  Alone, two
+  // 2^20 sets in one grid accumulate in 1.70 ms per set vs 1.96 for one
+  // (profiles/r05_acc_rate.txt: a launch's last waves leave the chip half
+  // idle), but in the batch the front and level 0 beside it fill that tail:
+  // groups of 2 per launch measured 427 vs 431-433 M pairs/s with H2D, the
+  // in-batch accumulation 1.75-1.80 vs 1.72-1.77 ms per set, profiles/r05_head_front_group_ab.txt)
   const size_t fg_max = !packed ? 1 : fg_env ? fg_env : acc_groups ? 4 : nl >= 3 ? 4 : nl == 2 ? 2 : (size_t)kFrontGroupDefault;
-  const bool acc_groups1 = nl < 2 && nseg == 1 && acc_group_env && fg_max > 1;
   // front groups of 1, 1, 2, 4, then fg_max MSMs: the first accumulation
   // starts after one front, and each group's host sets (copied while the earlier
   // groups accumulate: a set copies in ~0.6 ms, an MSM accumulates in ~2.3) are
@@ -1026,7 +1026,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
   // every buffer the loop touches exists before the first launch (an allocation
   // inside the issue loop could synchronise the device)
   const size_t NB = bucket_count(), n = n_;
-  if (acc_groups || acc_groups1)
+  if (acc_groups)
     for (DevBuf &b : gbuckets_) b.ensure(fg_max * NB * sizeof(Xyzz<typename FieldOf<G>::F>));
   else
     for (int b = 0; b < std::max(kBSets, nl); ++b) buckets_[b].ensure(NB * sizeof(Xyzz<typename FieldOf<G>::F>));
@@ -1350,46 +1350,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
     MSM_HIP_CHECK(hipEventRecord(evh[p], s));
     l0_group_tail(p);
   }
-  // One lane, accumulation groups: front group g's sets accumulate in ONE launch
-  // on the caller's stream into gbuckets_[g % 2] (after group g - 2's level 0s
-  // released it, and -- the level-0 wait -- after group g - 1's); each part of
-  // the group in reduction group q runs its level 0s in one launch on tails_[q % 2],
-  // followed there by q's tail when q ends inside the group.
-  for (size_t g = 0; g < (acc_groups1 && !fuse ? nfg : 0); ++g) {
-    copy_group(g + nsg);
-    const size_t k0 = fgb[g], k1 = fgb[g + 1];
-    const int gb = (int)(g & 1);
-    MSM_HIP_CHECK(hipStreamWaitEvent(s, evf[g], 0));
-    // every level 0 of group g - 2 (gbuckets_[gb] free again) and, the level-0
-    // wait, of group g - 1 (a group straddling two reduction groups ran its
-    // level 0s on both tail streams)
-    if (g >= 2)
-      for (size_t k = fgb[g - 2]; k < fgb[g - 1]; ++k) MSM_HIP_CHECK(hipStreamWaitEvent(s, evh[k], 0));
-    if (l0_first && g >= 1)
-      for (size_t k = fgb[g - 1]; k < k0; ++k) MSM_HIP_CHECK(hipStreamWaitEvent(s, evh[k], 0));
-    if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k0], s));
-    accumulate_sets(s, (int)(g % nfr), (int)(k1 - k0), gb, job_table(k0));
-    if (prof) {
-      MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k0 + 1], s));
-      prof_k.push_back(k0);
-    }
-    for (size_t k = k0; k < k1; ++k) MSM_HIP_CHECK(hipEventRecord(eva[k], s));
-    for (size_t a = k0; a < k1;) {
-      const size_t q = a / R, b = std::min(k1, (q + 1) * R);
-      hipStream_t ts = tails_[q % 2];
-      MSM_HIP_CHECK(hipStreamWaitEvent(ts, eva[k1 - 1], 0));
-      red.launch_head_slots(ts, gbuckets_[gb].as<uint8_t>() + (a - k0) * NB * sizeof(Xyzz<typename FieldOf<G>::F>), NB,
-                            (int)(q % 2), (int)(a % R), (int)(b - a));
-      for (size_t k = a; k < b; ++k) MSM_HIP_CHECK(hipEventRecord(evh[k], ts));
-      if (b % R == 0 || b == count) {  // reduction group q ends here
-        red.launch_tail_group(ts, (int)(q % 2), (int)(b - q * R), tail_coop && b == count);
-        red.copy_out_group(ts, (int)(q % 2), (int)(b - q * R), (uint8_t *)host_out_ + q * R * ob);
-      }
-      a = b;
-    }
-    issue_fronts(g + nfr - 1);
-  }
-  for (size_t g = 0; g < (nl >= 2 || fuse || acc_groups1 ? 0 : nfg); ++g) {
+  for (size_t g = 0; g < (nl >= 2 || fuse ? 0 : nfg); ++g) {
     copy_group(g + nsg);
     MSM_HIP_CHECK(hipStreamWaitEvent(s, evf[g], 0));
     for (size_t k = fgb[g]; k < fgb[g + 1]; ++k) {

@@ -440,7 +440,7 @@ class Ches {
   // 8 measured +1.2 % (profiles/r04_red_group_ab.txt).  MSM_RED_GROUP overrides.
   static constexpr int kGroup = 20;
   static constexpr int kFrontGroup = 8;  // batch: largest front group (ramping up 1, 1, 2, 4, 8)
-  static constexpr int kFrontGroupDefault = 2;  // one-lane batch: sets per front / accumulation group
+  static constexpr int kFrontGroupDefault = 1;
   // front k+1 may start when accumulation k-2 ends (slack for the copies); the
   // lane schedule of small MSMs rotates kFrontsMax sets (fronts further ahead)
   static constexpr int kFronts = 3, kFrontsMax = 5;
