@@ -268,6 +268,9 @@ int msm_ches_ctx_create_params(msm_ches_ctx **ctx, int group, int device, const 
  * table rows and scalars must be in host memory when ndev > 1. */
 int msm_ches_ctx_create_multi(msm_ches_ctx **ctx, int group, const int *devices, int ndev, int n_exp, int beta);
 int msm_ches_ctx_shards(const msm_ches_ctx *ctx);
+/* 1 if this context's batches exchange their partials over RCCL (several
+ * distinct devices, or MSM_MULTI_RCCL=1), 0 if each shard is read back */
+int msm_ches_ctx_rccl_exchange(const msm_ches_ctx *ctx);
 /* base points P_i (blst affine) -> T built on the GPU */
 int msm_ches_ctx_build_table(msm_ches_ctx *ctx, const void *points_affine, size_t npoints, int on_device,
                              void *hip_stream);

@@ -71,6 +71,7 @@ def lib():
     L.msm_register_host_table.argtypes = [i32, vp, sz]
     L.msm_unregister_host_table.argtypes = [vp]
     L.msm_ches_ctx_batch_lanes.argtypes = [vp]
+    L.msm_ches_ctx_rccl_exchange.argtypes = [vp]
     L.msm_ches_ctx_time_accumulation.argtypes = [vp, vp, sz, i32, i32, vp]
     L.msm_ches_ctx_destroy.argtypes = [vp]
     L.msm_ches_ctx_destroy.restype = None

@@ -71,7 +71,8 @@ def build(verbose=False, jobs=5):
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         list(ex.map(run, jobs_list))
     if jobs_list or _stale(LIB, objs):
-        run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", LIB] + objs)
+        # RCCL: the multi-device CHES batches gather their partials with ncclGather (csrc/multi.hpp)
+        run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", LIB] + objs + ["-L/opt/rocm/lib", "-lrccl"])
     if _VAR:
         return LIB
     # the reference-driver executables (ref main_p1.cpp / main_p2.cpp), host C++ on the C ABI

@@ -861,6 +861,8 @@ int msm_ches_ctx_shards(const msm_ches_ctx *ctx) {
 
 #define CHES_DISPATCH(ctx, CALL) ((ctx)->group == 1 ? (ctx)->g1->CALL : (ctx)->g2->CALL)
 
+int msm_ches_ctx_rccl_exchange(const msm_ches_ctx *ctx) { return ctx ? (int)CHES_DISPATCH(ctx, rccl_exchange()) : 0; }
+
 // several engines take host memory only (each device gets its own slice); shards
 // merged into one engine on one device (multi.hpp) take device memory like a
 // single-device context

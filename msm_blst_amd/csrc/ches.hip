@@ -487,7 +487,8 @@ void WeightedReducer<G>::launch_tail_group(hipStream_t s, int set, int nmsm, boo
 
 template <int G>
 void WeightedReducer<G>::copy_out_group(hipStream_t s, int set, int nmsm, void *host) {
-  MSM_HIP_CHECK(hipMemcpyAsync(host, dense_[set].fin.p, (size_t)nmsm * out_bytes(), hipMemcpyDeviceToHost, s));
+  // host (read-back) or device (an exchange buffer, ChesMulti's RCCL gather)
+  MSM_HIP_CHECK(hipMemcpyAsync(host, dense_[set].fin.p, (size_t)nmsm * out_bytes(), hipMemcpyDefault, s));
 }
 
 template <int G>
@@ -913,7 +914,8 @@ void Ches<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, hfp::J
 
 template <int G>
 void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, size_t set_stride, size_t nsets,
-                       size_t nseg, const void *const *tables, hfp::Jac<HF> *outs, bool scalars_on_host) {
+                       size_t nseg, const void *const *tables, hfp::Jac<HF> *outs, bool scalars_on_host,
+                       void *dev_out) {
   DeviceGuard g(dev_);
   if (stride < 32) throw std::runtime_error("CHES scalars must be 32-byte strings");
   if (nseg < 1) throw std::runtime_error("run_jobs: no segments");
@@ -983,6 +985,10 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
     MSM_HIP_CHECK(hipHostMalloc(&host_out_, bytes, hipHostMallocDefault));
     host_out_bytes_ = bytes;
   }
+  // where the groups' window sums land: the pinned read-back slots, or the
+  // caller's device exchange buffer (dev_out: ChesMulti gathers it over RCCL
+  // and combines on the host; the combine below is then skipped)
+  uint8_t *const out_base = dev_out ? static_cast<uint8_t *>(dev_out) : static_cast<uint8_t *>(host_out_);
   // (group size cap: kFrontGroupDefault, or MSM_FRONT_GROUP=<1..8>; engine.hpp)
   // (small MSMs on lanes: groups of 2 on two lanes -- half the front launches,
   // measured 0.551 -> 0.530 ms per 2^17 MSM and 0.874 -> 0.845 at 2^18 -- and 4
@@ -1258,7 +1264,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
         MSM_HIP_CHECK(hipStreamWaitEvent(ts, evh[k], 0));  // this lane's level 0s of group q
         if (k0 >= 1 && k0 - 1 >= first) MSM_HIP_CHECK(hipStreamWaitEvent(ts, evh[k0 - 1], 0));  // the other lane's
         red.launch_tail_group(ts, (int)(q % nred), (int)(k - first + 1), tail_coop && k + 1 == count);
-        red.copy_out_group(ts, (int)(q % nred), (int)(k - first + 1), (uint8_t *)host_out_ + first * ob);
+        red.copy_out_group(ts, (int)(q % nred), (int)(k - first + 1), out_base + first * ob);
         MSM_HIP_CHECK(hipEventRecord(evt[q], ts));
       }
       issue_fronts(g + nfr - 1);
@@ -1287,7 +1293,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
         if ((size_t)slot + 1 == R || k + 1 == count) {  // the group's level 0s are done on both lanes
           for (int d = 0; d < nl && d <= slot; ++d) MSM_HIP_CHECK(hipStreamWaitEvent(ts, evh[k - d], 0));
           red.launch_tail_group(ts, gset, slot + 1, tail_coop && k + 1 == count);
-          red.copy_out_group(ts, gset, slot + 1, (uint8_t *)host_out_ + (k - slot) * ob);
+          red.copy_out_group(ts, gset, slot + 1, out_base + (k - slot) * ob);
           MSM_HIP_CHECK(hipEventRecord(evt[q], ts));
         }
       }
@@ -1312,7 +1318,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
     hipStream_t ts = tails_[pq % 2];
     MSM_HIP_CHECK(hipStreamWaitEvent(ts, evh[p], 0));
     red.launch_tail_group(ts, (int)(pq % 2), (int)pslot + 1, tail_coop && p + 1 == count);
-    red.copy_out_group(ts, (int)(pq % 2), (int)pslot + 1, (uint8_t *)host_out_ + (p - pslot) * ob);
+    red.copy_out_group(ts, (int)(pq % 2), (int)pslot + 1, out_base + (p - pslot) * ob);
     MSM_HIP_CHECK(hipEventRecord(evt[pq], ts));
   };
   auto l0_set_free = [&](size_t p) {  // level 0 of MSM p may write its reducer set
@@ -1370,7 +1376,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
       MSM_HIP_CHECK(hipEventRecord(evh[k], ts));
       if ((size_t)slot + 1 == R || k + 1 == count) {  // the reduction group's last MSM
         red.launch_tail_group(ts, gset, slot + 1, tail_coop && k + 1 == count);
-        red.copy_out_group(ts, gset, slot + 1, (uint8_t *)host_out_ + (k - slot) * ob);
+        red.copy_out_group(ts, gset, slot + 1, out_base + (k - slot) * ob);
       }
     }
     issue_fronts(g + nfr - 1);
@@ -1387,7 +1393,9 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
   // the per-MSM host Horner (~20 us each) over the host worker threads: with
   // one reduction group per batch every combine runs after the last tail
   auto combine_k = [&](size_t k) { outs[k] = red.combine((const uint8_t *)host_out_ + k * ob)[0]; };
-  if (count >= 4) {
+  if (dev_out) {
+    // the window sums stay in dev_out for the caller's exchange
+  } else if (count >= 4) {
     WorkerPool::get().parallel_for(count, combine_k);
   } else {
     for (size_t k = 0; k < count; ++k) combine_k(k);

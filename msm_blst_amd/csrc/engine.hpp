@@ -383,18 +383,24 @@ class Ches {
   // + sort of up to kFrontGroup sets in one pass) beside group g's
   // accumulations, MSM k's reduction on a second stream beside MSM k+1's
   // accumulation.
+  // dev_out (device memory of this engine's device, count * exchange_bytes()):
+  // the per-MSM window sums are left there instead of being read back and
+  // combined (outs untouched) -- ChesMulti's RCCL exchange
   void run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, size_t set_stride, size_t count,
-                 hfp::Jac<HF> *outs, bool scalars_on_host = false) {
+                 hfp::Jac<HF> *outs, bool scalars_on_host = false, void *dev_out = nullptr) {
     const void *t = table_.p;
-    run_jobs(s, scalars, stride, set_stride, count, 1, &t, outs, scalars_on_host);
+    run_jobs(s, scalars, stride, set_stride, count, 1, &t, outs, scalars_on_host, dev_out);
   }
+  // bytes of one MSM's window sums in a batch exchange buffer, and their combine
+  size_t exchange_bytes() const { return batch_red_->out_bytes(); }
+  hfp::Jac<HF> combine_exchange(const void *host) const { return batch_red_->combine(host)[0]; }
   // The batch over nseg point segments of n_ points each, one pipeline: segment
   // d's table is tables[d] (engines of the same parameters and n on this
   // device, e.g. the shards of a multi-shard context that share a GPU), its
   // scalars the d-th n-string slice of every set.  outs: count * nseg partial
   // Jacobians, job k nseg + d = (set k, segment d).
   void run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, size_t set_stride, size_t count, size_t nseg,
-                const void *const *tables, hfp::Jac<HF> *outs, bool scalars_on_host);
+                const void *const *tables, hfp::Jac<HF> *outs, bool scalars_on_host, void *dev_out = nullptr);
   const void *table_ptr() const { return table_.p; }
   size_t npoints() const { return n_; }
   const ChesParams &params() const { return p_; }

@@ -14,11 +14,19 @@
 // thread per shard per call was a visible fixed cost at 2^18 points per GPU,
 // where one MSM takes < 1 ms), and host scalars reach each device through the
 // shard's pinned ring (hoststage.hpp) instead of a pageable copy.
-// No device-to-device traffic is needed: the partials reach host memory with
-// the per-MSM read-back every shard does anyway, so a collective (RCCL) would
-// only add a hop for 144 bytes.  The reference itself is single-device; its Go
-// binding splits points x windows over threads (bindings/go/blst.go:2064-2197),
-// which would replicate points and tables on every GPU, so points are sharded.
+// Batches on several DISTINCT devices exchange over RCCL (the north star's
+// "single RCCL reduce of the partial sums over xGMI"): every shard leaves its
+// per-MSM window sums (2 Jacobians, 288 B G1 / 576 B G2, per MSM) in a device
+// exchange buffer, ONE ncclGather collects all shards' buffers on the first
+// shard's device, one read-back, and the host combines and folds them exactly
+// (RCCL's reduction ops cannot add curve points, hence gather + fold).
+// MSM_MULTI_RCCL=0 reads every shard back separately instead (host fold of
+// the shards' own read-backs); =1 forces the RCCL exchange for any context of
+// distinct devices, including a single shard (how one GPU tests it).  Single
+// MSMs (run) keep the per-shard read-back: their latency path.  The reference
+// itself is single-device; its Go binding splits points x windows over threads
+// (bindings/go/blst.go:2064-2197), which would replicate points and tables on
+// every GPU, so points are sharded.
 //
 // Shards may share a device (devices = {0, 0, ...}).  Consecutive shards on one
 // device are merged into ONE engine over their joint point range (the table
@@ -39,6 +47,8 @@
 #include <mutex>
 #include <thread>
 #include <vector>
+
+#include <rccl/rccl.h>
 
 #include "engine.hpp"
 #include "hoststage.hpp"
@@ -99,7 +109,10 @@ class ChesMulti {
       throw;
     }
   }
-  ~ChesMulti() { release(); }
+  ~ChesMulti() {
+    release();
+    for (ncclComm_t c : comms_) (void)ncclCommDestroy(c);
+  }
   ChesMulti(const ChesMulti &) = delete;
   ChesMulti &operator=(const ChesMulti &) = delete;
   size_t nshards() const { return nlogical_; }  // the caller's shards (merged ones included)
@@ -183,6 +196,7 @@ class ChesMulti {
   // several shards); every shard runs its own pipelined batch on its slice
   void run_batch(hipStream_t s, const uint8_t *scalars, size_t stride, size_t set_stride, size_t count,
                  hfp::Jac<HF> *outs, bool on_host) {
+    if (use_rccl()) return run_batch_rccl(s, scalars, stride, set_stride, count, outs, on_host);
     if (shards_.size() == 1) return shards_[0].eng->run_batch(s, scalars, stride, set_stride, count, outs, on_host);
     if (!on_host) throw std::runtime_error("multi-device mult_batch takes host scalars");
     if (one_device_pipeline()) {
@@ -222,6 +236,7 @@ class ChesMulti {
   void set_profiling(bool on) {
     for (Shard &sh : shards_) sh.eng->set_profiling(on);
   }
+  bool rccl_exchange() const { return use_rccl(); }
 
  private:
   ChesParams p_;
@@ -253,6 +268,102 @@ class ChesMulti {
   }
   std::vector<Worker> workers_;  // one per shard when there are several
   std::mutex each_mu_;           // one each() at a time per context
+  // RCCL exchange of batch partials (use_rccl): one communicator per shard
+  // device (ncclCommInitAll, created at the first exchange), the shards' send
+  // buffers and the gather buffer on shard 0's device
+  std::vector<ncclComm_t> comms_;
+  std::vector<DevBuf> xsend_;
+  DevBuf xrecv_;
+  std::vector<hipStream_t> xstreams_;  // the shards' streams (created here for a single shard)
+
+  bool use_rccl() const {
+    static const int env = [] {
+      const char *e = getenv("MSM_MULTI_RCCL");
+      return e ? atoi(e) : -1;
+    }();
+    if (env == 0 || shards_.empty()) return false;
+    for (size_t a = 0; a < shards_.size(); ++a)  // distinct devices only (one rank per device)
+      for (size_t b = a + 1; b < shards_.size(); ++b)
+        if (shards_[a].device == shards_[b].device) return false;
+    return env == 1 || shards_.size() > 1;
+  }
+  static void nccl_check(ncclResult_t r, const char *what) {
+    if (r != ncclSuccess) throw std::runtime_error(std::string("RCCL ") + what + ": " + ncclGetErrorString(r));
+  }
+  // every shard runs its batch into its send buffer (concurrently, one worker per
+  // shard), then one ncclGather onto shard 0's device, one read-back, and the
+  // host combine + fold per MSM in shard order
+  void run_batch_rccl(hipStream_t s, const uint8_t *scalars, size_t stride, size_t set_stride, size_t count,
+                      hfp::Jac<HF> *outs, bool on_host) {
+    if (!on_host && shards_.size() > 1) throw std::runtime_error("multi-device mult_batch takes host scalars");
+    const size_t D = shards_.size();
+    if (comms_.empty()) {
+      std::vector<int> devs(D);
+      for (size_t g = 0; g < D; ++g) devs[g] = shards_[g].device;
+      comms_.resize(D);
+      nccl_check(ncclCommInitAll(comms_.data(), (int)D, devs.data()), "ncclCommInitAll");
+      xsend_ = std::vector<DevBuf>(D);
+      xstreams_.assign(D, nullptr);
+      for (size_t g = 0; g < D; ++g) {
+        xstreams_[g] = shards_[g].stream;
+        if (!xstreams_[g]) {  // a single shard: its own stream for the collective
+          DeviceGuard dg(shards_[g].device);
+          MSM_HIP_CHECK(hipStreamCreateWithFlags(&shards_[g].stream, hipStreamNonBlocking));
+          xstreams_[g] = shards_[g].stream;
+        }
+      }
+    }
+    const size_t ob = shards_[0].eng->exchange_bytes();
+    for (size_t g = 0; g < D; ++g) {
+      DeviceGuard dg(shards_[g].device);
+      xsend_[g].ensure(count * ob);
+    }
+    {
+      DeviceGuard dg(shards_[0].device);
+      xrecv_.ensure(D * count * ob);
+    }
+    each([&](Shard &sh) {
+      const size_t g = &sh - shards_.data();
+      DeviceGuard dg(sh.device);
+      if (sh.n) {
+        std::vector<hfp::Jac<HF>> unused(1);
+        sh.eng->run_batch(sh.stream, scalars + sh.start * stride, stride, set_stride, count, unused.data(), on_host,
+                          xsend_[g].p);
+      } else {
+        MSM_HIP_CHECK(hipMemsetAsync(xsend_[g].p, 0, count * ob, sh.stream));  // all-zero Jacobians: infinity
+      }
+      MSM_HIP_CHECK(hipStreamSynchronize(sh.stream));
+    });
+    nccl_check(ncclGroupStart(), "ncclGroupStart");
+    for (size_t g = 0; g < D; ++g) {
+      DeviceGuard dg(shards_[g].device);
+      nccl_check(ncclGather(xsend_[g].p, g == 0 ? xrecv_.p : nullptr, count * ob, ncclUint8, 0, comms_[g],
+                            shards_[g].stream),
+                 "ncclGather");
+    }
+    nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+    std::vector<uint8_t> host(D * count * ob);
+    {
+      DeviceGuard dg(shards_[0].device);
+      MSM_HIP_CHECK(hipMemcpyAsync(host.data(), xrecv_.p, host.size(), hipMemcpyDeviceToHost, shards_[0].stream));
+      for (size_t g = 0; g < D; ++g) {
+        DeviceGuard dg2(shards_[g].device);
+        MSM_HIP_CHECK(hipStreamSynchronize(shards_[g].stream));
+      }
+    }
+    (void)s;
+    for (size_t k = 0; k < count; ++k) {
+      std::vector<hfp::Jac<HF>> col(D);
+      for (size_t g = 0; g < D; ++g) {
+        const uint8_t *w = host.data() + (g * count + k) * ob;
+        bool zero = true;  // a shard without points sent zeros (infinity)
+        for (size_t b = 0; b < ob && zero; ++b) zero = w[b] == 0;
+        if (zero) std::memset(&col[g], 0, sizeof col[g]);
+        else col[g] = shards_[g].eng->combine_exchange(w);
+      }
+      outs[k] = fold(col);
+    }
+  }
 
   static void work(Worker &w) {
     for (;;) {

@@ -56,3 +56,43 @@ def test_rccl_world1_gather_and_fold(golden):
     assert d["world"] == 1 and d["max"] == 1.5
     assert d["set0"] == want
     assert all(d["same"])
+
+
+CHILD_MULTI = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+import msm_blst_amd as m
+out = []
+for group, n_exp, K in ((1, 16, 4), (2, 10, 3)):
+    n = 1 << n_exp
+    ctx = m.CHESContext(group, n_exp=n_exp, devices=[0])
+    ctx.build_table(m.fixed_points(group, n), n)
+    sets = b"".join(bytes(m.gen_scalars(n, 1 if k == 0 else 60 + k)) for k in range(K))
+    got = [m.compress(group, r).hex() for r in ctx.mult_batch(sets, K)]
+    want = [m.compress(group, ctx.mult(sets[32 * n * k:32 * n * (k + 1)])).hex() for k in range(K)]
+    out.append((group, got[0], got == want, m.lib().msm_ches_ctx_rccl_exchange(ctx._ctx)))
+    ctx.close()
+print("RESULT", out)
+"""
+
+
+def test_c_abi_multi_device_rccl_gather(golden):
+    """The C-ABI multi-device batch exchanging over RCCL (csrc/multi.hpp
+    run_batch_rccl: every shard's window sums into a device exchange buffer, ONE
+    ncclGather onto the first shard's device, one read-back, host combine +
+    fold), forced with MSM_MULTI_RCCL=1 on a one-device context (a communicator
+    of one rank: the gather is a device copy).  Set 0 against the golden keys,
+    every set against the synchronous MSM."""
+    want = {g: [c["compressed"] for c in golden(f"msm_g{g}.json")["cases"]
+                if c["n"] == n and c["seed"] == 1 and c["case"] == "rand" and c["nbits"] == 255][0]
+            for g, n in ((1, 1 << 16), (2, 1 << 10))}
+    env = dict(os.environ, MSM_MULTI_RCCL="1")
+    r = subprocess.run([sys.executable, "-c", CHILD_MULTI, REPO], capture_output=True, text=True, env=env, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")]
+    assert line, r.stdout[-2000:] + r.stderr[-2000:]
+    res = eval(line[0][7:])  # noqa: S307 -- our own child's repr of tuples of str/bool/int
+    for group, set0, same, rccl in res:
+        assert rccl == 1, "the RCCL exchange was not selected"
+        assert set0 == want[group]
+        assert same

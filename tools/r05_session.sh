@@ -27,6 +27,7 @@ for step in "$@"; do
            cat $O/trace.txt; python3 tools/batch_profile.py $O/trace/run_kernel_trace.csv > $O/trace_profile.txt; cat $O/trace_profile.txt ;;
     shards_acc) timeout -k 10 300 python -u tools/shard_study.py --cfgs 20,19 > $O/shards_acc.txt 2> $O/shards_acc.err && MSM_FRONT_PHASE=0 timeout -k 10 300 python -u tools/shard_study.py --cfgs 20 >> $O/shards_acc.txt 2>> $O/shards_acc.err && MSM_FRONT_GROUP=8 timeout -k 10 300 python -u tools/shard_study.py --cfgs 20,19 >> $O/shards_acc.txt 2>> $O/shards_acc.err; rc=$?; cat $O/shards_acc.txt ;;
     abitests) timeout -k 10 400 python -u -m pytest tests/test_gpu_blst_ches_abi.py tests/test_gpu_tile_grid.py tests/test_gpu_dropin.py tests/test_gpu_pointer_gather.py tests/test_gpu_parity.py -x -v --timeout 300 --timeout-method thread > $O/pytest_abi.txt 2>&1; rc=$?; tail -3 $O/pytest_abi.txt ;;
+    rccltests) timeout -k 10 400 python -u -m pytest tests/test_gpu_rccl.py tests/test_gpu_multi.py -x -v --timeout 300 --timeout-method thread > $O/pytest_rccl.txt 2>&1; rc=$?; tail -5 $O/pytest_rccl.txt ;;
     batchtests) timeout -k 10 500 python -u -m pytest tests/test_gpu_ches.py tests/test_gpu_batch_one_lane.py tests/test_gpu_multi.py -x -v --timeout 300 --timeout-method thread > $O/pytest_batch.txt 2>&1; rc=$?; tail -3 $O/pytest_batch.txt ;;
     tile) timeout -k 10 300 python -u tools/tile_timing.py > $O/tile.txt 2> $O/tile.err; rc=$?; cat $O/tile.txt; grep "\[tile\]" $O/tile.err ;;
     rehearse) for N in 2 4 8; do
