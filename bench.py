@@ -552,7 +552,7 @@ def config_legs(m, torch, dev, local, sp, pts, host, K, W):
             "note": f"configs[1]: K synchronous msm_ctx_mult calls (per-MSM latency), window c={c}, points and "
                     f"{K} scalar sets resident in HBM"}
         # the same K sets through the pipelined batch (msm_ctx_mult_batch): throughput
-        pc.mult_batch(d16.data_ptr(), min(max(W, 1), K), 255, on_device=True, stream=sp)
+        pc.mult_batch(d16.data_ptr(), K, 255, on_device=True, stream=sp)  # untimed: sizes the batch buffers
         torch.cuda.synchronize(dev)
         t = time.perf_counter()
         rb = pc.mult_batch(d16.data_ptr(), K, 255, on_device=True, stream=sp)
@@ -562,9 +562,10 @@ def config_legs(m, torch, dev, local, sp, pts, host, K, W):
             "value": round(n16 * K / elb, 1), "unit": "pairs/s", "ms_per_step": round(elb / K * 1e3, 4),
             "parity_vs_reference": m.compress(1, rb[0]).hex() == want16,
             "batch_equals_sync": [m.compress(1, x) for x in rb] == [m.compress(1, x) for x in r],
-            "note": f"configs[1]: one msm_ctx_mult_batch call over the same {K} resident sets, window c={c}: front "
-                    f"k+2 beside accumulation k, two accumulation lanes, grouped reduction tails, host Horner of "
-                    f"group q beside the GPU work of later groups"}
+            "note": f"configs[1]: one msm_ctx_mult_batch call over the same {K} resident sets, window c={c}, after "
+                    f"one untimed batch of {K}: fronts in groups of up to 4 sets, one accumulation launch per "
+                    f"group on two lanes, grouped reduction tails, host Horner of group q beside the GPU work "
+                    f"of later groups"}
         pc.close()
     for _ in range(max(W, 1)):
         dropin(1, P16, sets16[0], n16)

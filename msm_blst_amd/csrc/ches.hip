@@ -1141,7 +1141,16 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
   std::vector<size_t> prof_k;  // profiling: acc_ev_ pairs recorded (per MSM, or per accumulation group)
   MSM_HIP_CHECK(hipEventRecord(bev_[0], s));  // the batch starts after prior work on s
   MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, bev_[0], 0));
-  MSM_HIP_CHECK(hipStreamWaitEvent(cstream_, bev_[0], 0));
+  // The copy stream does NOT wait on the batch-start event: an SDMA copy
+  // enqueued behind a cross-stream event wait now and then blocked the issuing
+  // thread -- the one that enqueues the whole pipeline -- for 7-9 ms (rocprofv3
+  // HIP API traces of bench.py: the batch's second hipMemcpyAsync took 7.4 ms in
+  // 3 of 5 traced runs, the GPU idle meanwhile; tools/microbench/copy_block.hip:
+  // blocked calls only with the wait; profiles/r05_h2d_block.txt).  Prior work
+  // on the caller's stream (which may write the host sets) is awaited on the
+  // host instead; the device slots are only read by this engine's batches,
+  // which end synchronised.
+  if (scalars_on_host) MSM_HIP_CHECK(hipEventSynchronize(bev_[0]));
   for (int t = 0; t < kBSets; ++t) MSM_HIP_CHECK(hipStreamWaitEvent(tails_[t], bev_[0], 0));
   auto slots = [&](size_t g) { return scal_.as<uint8_t>() + (g % nsg) * fg_max * sslot; };
   // MSM_ZERO_COPY_SCALARS=1 (A/B knob): page-locked host sets are read by the

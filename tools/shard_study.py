@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--logs", default="17,18,19")
     ap.add_argument("--cfgs", default="22,20,19,18,16")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--all", action="store_true", help="also print every repetition's ms per MSM")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -52,9 +53,10 @@ def main():
             torch.cuda.synchronize(dev)
             setup = time.time() - t
             ctx.mult_batch(host.data_ptr(), 3, 32, set_stride=n * 32, on_device=False, stream=sp)
-            res = {}
+            res, every = {}, {}
             for mode, ptr, on_dev in (("resident", d.data_ptr(), True), ("h2d", host.data_ptr(), False)):
                 best = None
+                every[mode] = []
                 for _ in range(a.reps):
                     torch.cuda.synchronize(dev)
                     t = time.perf_counter()
@@ -62,12 +64,15 @@ def main():
                     torch.cuda.synchronize(dev)
                     el = (time.perf_counter() - t) / K * 1e3
                     best = el if best is None else min(best, el)
+                    every[mode].append(round(el, 4))
                 res[mode] = round(best, 4)
             keys[qe] = m.compress(1, out[0]).hex()
             p = ctx.params
             line = {"log_n": lg, "q_exp": qe, "h": p["h"], "b_size": p["b_size"], "lanes": ctx.batch_lanes(),
                     "buckets": ctx.bucket_count(), "ms_resident": res["resident"], "ms_h2d": res["h2d"],
                     "setup_s": round(setup, 2)}
+            if a.all:
+                line["every"] = every
             ctx.close()
             print(json.dumps(line), flush=True)
         print(json.dumps({"log_n": lg, "all_configs_agree": len(set(keys.values())) == 1}), flush=True)
