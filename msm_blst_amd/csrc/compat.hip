@@ -65,9 +65,13 @@ struct EntryMsmState {
   PinnedBuf hkv, hring, hbx;      // pinned: keys + vals, the point-row ring, exported buckets
   HeavyScratch heavy;             // heavy buckets split over several lanes (heavy.hpp)
   hipEvent_t ring_ev[4] = {};
+  hipStream_t up = nullptr;  // row uploads: beside the sort on the lease's stream
+  hipEvent_t up_ev = nullptr;
   ~EntryMsmState() {
     for (hipEvent_t &e : ring_ev)
       if (e) (void)hipEventDestroy(e);
+    if (up_ev) (void)hipEventDestroy(up_ev);
+    if (up) (void)hipStreamDestroy(up);
   }
   size_t device_bytes() const {  // device buffers + pinned staging (the pool's idle budget counts both)
     size_t b = hkv.bytes + hring.bytes + hbx.bytes;
@@ -122,7 +126,19 @@ struct TileClock {
 
 template <int G, class PT>
 static void entry_msm_back(EntryMsmState<G> &S, hipStream_t s, const PT *pts, void *ret, size_t ne, size_t nb,
-                           const uint32_t *weights, void *buckets_out, bool pinned_export, TileClock *clk = nullptr);
+                           const uint32_t *weights, void *buckets_out, bool pinned_export, TileClock *clk = nullptr,
+                           bool presorted = false);
+
+// bucket sort of the entries in S.keys / S.vals (counts, offsets, schedule)
+template <int G>
+static void entry_sort(EntryMsmState<G> &S, hipStream_t s, size_t ne, size_t nb) {
+  S.counts.ensure(nb * 4);
+  S.offsets.ensure(nb * 4);
+  S.order.ensure(nb * 4);
+  S.sort.run(s, S.keys.template as<uint32_t>(), S.vals.template as<uint32_t>(), ne, (uint32_t)nb,
+             S.sorted.template as<uint32_t>(), S.counts.template as<uint32_t>(), S.offsets.template as<uint32_t>(),
+             S.order.template as<uint32_t>());
+}
 
 template <int G>
 void entry_msm(void *ret, const void *pts_blst, size_t npts, const uint32_t *keys, const uint32_t *vals, size_t ne,
@@ -161,16 +177,13 @@ void entry_msm(void *ret, const void *pts_blst, size_t npts, const uint32_t *key
 // S.keys / S.vals over the point rows pts (S.pts, or a registered table)
 template <int G, class PT>
 static void entry_msm_back(EntryMsmState<G> &S, hipStream_t s, const PT *pts, void *ret, size_t ne, size_t nb,
-                           const uint32_t *weights, void *buckets_out, bool pinned_export, TileClock *clk) {
+                           const uint32_t *weights, void *buckets_out, bool pinned_export, TileClock *clk,
+                           bool presorted) {
   typedef typename FieldOf<G>::F F;
   typedef typename HostField<G>::F HF;
   hfp::Jac<HF> out;
-  S.counts.ensure(nb * 4);
-  S.offsets.ensure(nb * 4);
-  S.order.ensure(nb * 4);
   S.buckets.ensure(nb * sizeof(Xyzz<F>));
-  S.sort.run(s, S.keys.template as<uint32_t>(), S.vals.template as<uint32_t>(), ne, (uint32_t)nb, S.sorted.template as<uint32_t>(),
-             S.counts.template as<uint32_t>(), S.offsets.template as<uint32_t>(), S.order.template as<uint32_t>());
+  if (!presorted) entry_sort(S, s, ne, nb);
   // the caller's entries as they come: the CHES top digit's few buckets hold
   // n entries between them, so heavy buckets are split over several lanes
   launch_accumulate_heavy<G>(s, S.sort.sched(S.order.template as<uint32_t>(), S.sorted.template as<uint32_t>(), 0, nb),
@@ -265,14 +278,33 @@ void entry_msm_ptrs(void *ret, const void *const *points, size_t ne, EntryFill f
     entry_msm_back<G>(S, s, tab->rows.template as<AffP<F>>(), ret, ne, nb, weights, buckets_out, true, &clk);
     return;
   }
+  // the sort needs only keys / vals: it runs on the GPU while the host gathers
+  entry_sort(S, s, ne, nb);
   // point rows: gathered chunk by chunk into a 4-slot pinned ring (the host
-  // gather of chunk c + 1 overlaps the DMA of chunk c), converted on the device
-  // 4 slots of at most 32 MiB: the ring is 128 MiB of page-locked memory
-  // whatever ne (ne / 16 rows per slot kept ~300 MB / 600 MB pinned per pooled
-  // state for a 2^20 G1 / G2 tile); a 2^20 tile goes ~36 times
-  // around the ring
+  // gather of chunk c + 1 overlaps the DMA of chunk c), uploaded and converted
+  // on a second stream (not queued behind the sort), which the accumulation
+  // waits for.  4 slots of at most 32 MiB: the ring is 128 MiB of page-locked
+  // memory whatever ne (ne / 16 rows per slot kept ~300 MB / 600 MB pinned per
+  // pooled state for a 2^20 G1 / G2 tile); smaller slots made the
+  // host wait for the DMA more often (8 MiB: 2^16 tile 5.77 vs 5.46 ms, 2^20
+  // 53 vs 50 ms; profiles/r05_tile_timing.txt).  The upload stream needs no
+  // wait on the lease's stream: the lease synchronised it above, and a copy
+  // enqueued behind a cross-stream wait can block the host
+  // (profiles/r05_h2d_block.txt).
   constexpr int kSlots = 4;
-  const size_t chunk = std::min(ne, ((size_t)32 << 20) / psz);
+  if (!S.up) {
+    MSM_HIP_CHECK(hipStreamCreateWithFlags(&S.up, hipStreamNonBlocking));
+    MSM_HIP_CHECK(hipEventCreateWithFlags(&S.up_ev, hipEventDisableTiming));
+  }
+  static const size_t kRingSlotBytes = [] {  // A/B knob MSM_RING_SLOT_MIB
+    const char *e = getenv("MSM_RING_SLOT_MIB");
+    return (size_t)(e ? std::max(1, std::min(64, atoi(e))) : 32) << 20;
+  }();
+  static const size_t kGatherAhead = [] {  // A/B knob MSM_GATHER_AHEAD (rows; 0: no prefetch)
+    const char *e = getenv("MSM_GATHER_AHEAD");
+    return (size_t)(e ? std::max(0, std::min(256, atoi(e))) : 16);
+  }();
+  const size_t chunk = std::min(ne, (kRingSlotBytes) / psz);
   S.hring.ensure(chunk * psz * kSlots);
   for (hipEvent_t &e : S.ring_ev)
     if (!e) MSM_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -286,17 +318,27 @@ void entry_msm_ptrs(void *ret, const void *const *points, size_t ne, EntryFill f
     const size_t sub = std::max<size_t>(4096, (cnt + 15) / 16);
     WorkerPool::get().parallel_for((cnt + sub - 1) / sub, [&](size_t j) {
       const size_t a = j * sub, b = std::min(cnt, a + sub);
-      for (size_t t = a; t < b; ++t) std::memcpy(slot + t * psz, points[c0 + t], psz);
+      // random row reads: prefetch kGatherAhead rows ahead (both 64-B lines of
+      // a G1 row) to keep more DRAM misses in flight per thread
+      for (size_t t = a; t < b; ++t) {
+        if (kGatherAhead && t + kGatherAhead < b) {
+          const char *q = static_cast<const char *>(points[c0 + t + kGatherAhead]);
+          for (size_t l = 0; l < psz; l += 64) __builtin_prefetch(q + l);
+        }
+        std::memcpy(slot + t * psz, points[c0 + t], psz);
+      }
     });
-    MSM_HIP_CHECK(hipMemcpyAsync(S.xfer.template as<uint8_t>() + c0 * psz, slot, cnt * psz, hipMemcpyHostToDevice, s));
-    MSM_HIP_CHECK(hipEventRecord(S.ring_ev[k], s));
+    MSM_HIP_CHECK(hipMemcpyAsync(S.xfer.template as<uint8_t>() + c0 * psz, slot, cnt * psz, hipMemcpyHostToDevice, S.up));
+    MSM_HIP_CHECK(hipEventRecord(S.ring_ev[k], S.up));
     used[k] = true;
   }
-  hipLaunchKernelGGL(k_convert_points<G>, dim3(nblk(ne, 256)), dim3(256), 0, s, S.xfer.template as<uint64_t>(),
+  hipLaunchKernelGGL(k_convert_points<G>, dim3(nblk(ne, 256)), dim3(256), 0, S.up, S.xfer.template as<uint64_t>(),
                      S.pts.template as<Aff<F>>(), ne);
   MSM_HIP_CHECK(hipGetLastError());
+  MSM_HIP_CHECK(hipEventRecord(S.up_ev, S.up));
+  MSM_HIP_CHECK(hipStreamWaitEvent(s, S.up_ev, 0));
   clk.lap("gather");
-  entry_msm_back<G>(S, s, S.pts.template as<Aff<F>>(), ret, ne, nb, weights, buckets_out, true, &clk);
+  entry_msm_back<G>(S, s, S.pts.template as<Aff<F>>(), ret, ne, nb, weights, buckets_out, true, &clk, true);
 }
 
 template <int G>

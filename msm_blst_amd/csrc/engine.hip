@@ -471,10 +471,12 @@ void Pippenger<G>::run_host(hipStream_t s, const void *pts_blst, size_t n, const
   }
   if (!stage_) stage_ = std::make_unique<HostStager>();
   // the point upload (stream up_) must not overwrite points an earlier MSM on s
-  // still reads; recorded before this call's front so the upload overlaps the
-  // scalars' digits and sort instead of queueing behind them
+  // still reads: awaited on the host (an earlier call ended with its read-back,
+  // so this returns at once), not by a cross-stream wait -- copies enqueued
+  // behind such a wait now and then blocked the host for 7-9 ms
+  // (profiles/r05_h2d_block.txt).  The upload overlaps this call's digits + sort.
   MSM_HIP_CHECK(hipEventRecord(ev_s_, s));
-  MSM_HIP_CHECK(hipStreamWaitEvent(up_, ev_s_, 0));
+  MSM_HIP_CHECK(hipEventSynchronize(ev_s_));
   const size_t sbytes = n * stride;
   scal_.ensure(sbytes + (tile ? n * 5 : 0) + 16);
   stage_->upload(scal_.p, scalars, sbytes, s);

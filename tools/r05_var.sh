@@ -1,13 +1,12 @@
-# bench.py headline runs after removing the copy stream's cross-stream wait:
-# 5 runs under a HIP API trace (before: 3 of 5 and 7 of 8 traced runs slow) + 3 plain
+# tile: sort before the row gather, uploads on a second stream; ring slot size A/B; ABI tests
 set -o pipefail
-R=$(pwd); O=$R/gpurun_out/r05nw; mkdir -p $O
-export TMPDIR=/tmp
-for i in 1 2 3 4 5; do
-  (cd /tmp && timeout -k 10 150 rocprofv3 --kernel-trace --memory-copy-trace --hip-runtime-trace --output-format csv -d $O/t$i -o run -- python3 $R/bench.py --no-configs --no-shards --no-cpu-baseline --no-compare > $O/tb$i.json 2> $O/tb$i.err) || exit 1
-  python3 -c "import json; d=json.loads(open('$O/tb$i.json').read().strip().splitlines()[-1]); print('traced $i', d['value'], d['ms_per_step'], d['roofline']['kernel_ms'])" | tee -a $O/runs.txt
+O=gpurun_out/r05gb; mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests/test_gpu_blst_ches_abi.py tests/test_gpu_pointer_gather.py tests/test_gpu_dropin.py tests/test_gpu_tile_grid.py tests/test_gpu_driver.py -x -q --timeout 300 --timeout-method thread > $O/abi.txt 2>&1 || { tail -30 $O/abi.txt; exit 1; }
+tail -1 $O/abi.txt
+for env in "MSM_RING_SLOT_MIB=8" "MSM_RING_SLOT_MIB=32" "MSM_RING_SLOT_MIB=4" "MSM_RING_SLOT_MIB=8"; do
+  echo "## $env" >> $O/ga.txt
+  env $env timeout -k 10 300 python -u tools/tile_timing.py > $O/t.json 2> $O/t.err || exit 1
+  grep "\[tile\]" $O/t.err | awk 'NR==3 || NR==4 || NR==11 || NR==12' >> $O/ga.txt
+  python -c "import json; d=json.load(open('$O/t.json')); print({k: (v['ms_per_step'], v['ratio_vs_ctx_sync'], v['parity_vs_reference']) for k, v in d.items()})" >> $O/ga.txt
 done
-for i in 1 2 3; do
-  timeout -k 10 300 python -u bench.py --no-configs --no-cpu-baseline --no-shards > $O/b$i.json 2> $O/b$i.err || exit 1
-  python tools/bench_summary.py $O/b$i.json 2>&1 | sed -n 1,3p | tee -a $O/runs.txt
-done
+cat $O/ga.txt
