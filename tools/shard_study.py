@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--logs", default="17,18,19")
     ap.add_argument("--cfgs", default="22,20,19,18,16")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--warm", type=int, default=3, help="sets in the untimed warm-up batch")
     ap.add_argument("--all", action="store_true", help="also print every repetition's ms per MSM")
     a = ap.parse_args()
     import numpy as np
@@ -52,7 +53,7 @@ def main():
             ctx.build_table(pts, n, stream=sp)
             torch.cuda.synchronize(dev)
             setup = time.time() - t
-            ctx.mult_batch(host.data_ptr(), 3, 32, set_stride=n * 32, on_device=False, stream=sp)
+            ctx.mult_batch(host.data_ptr(), min(a.warm, K), 32, set_stride=n * 32, on_device=False, stream=sp)
             res, every = {}, {}
             for mode, ptr, on_dev in (("resident", d.data_ptr(), True), ("h2d", host.data_ptr(), False)):
                 best = None
