@@ -131,17 +131,21 @@ void ches_digit_code(const std::vector<int> &B, int q, std::vector<uint32_t> &co
 #endif  // MSM_GROUP == 1
 
 // a tail level of segment sums: few outputs are latency-bound, so one add
-// spreads over 4 waves (coop.hpp: G1 one lane per wave, G2 a lane pair per wave)
+// spreads over 4 waves (coop.hpp: G1 one lane per wave, G2 a lane pair per wave);
+// nmsm > 1: the MSMs of a batch group, src / dst advanced by their strides
 template <int G>
 static void launch_segsum_tail(hipStream_t s, const Xyzz<typename FieldOf<G>::F> *src, const uint32_t *ix,
-                               const uint32_t *st, Xyzz<typename FieldOf<G>::F> *dst, size_t nout, bool coop) {
-  if (coop && nout <= 16384) {
+                               const uint32_t *st, Xyzz<typename FieldOf<G>::F> *dst, size_t nout, bool coop,
+                               int nmsm = 1, size_t sstride = 0, size_t dstride = 0) {
+  if (coop && nout * (size_t)nmsm <= 16384) {
     if constexpr (G == 1)
-      hipLaunchKernelGGL(k_segsum_c<G>, dim3(nblk(nout, 64)), dim3(256), 0, s, src, ix, st, dst, nout);
+      hipLaunchKernelGGL(k_segsum_c<G>, dim3(nblk(nout, 64), (unsigned)nmsm), dim3(256), 0, s, src, ix, st, dst, nout,
+                         sstride, dstride);
     else
-      hipLaunchKernelGGL(k_segsum_c2p, dim3(nblk(nout, 32)), dim3(256), 0, s, src, ix, st, dst, nout);
+      hipLaunchKernelGGL(k_segsum_c2p, dim3(nblk(nout, 32), (unsigned)nmsm), dim3(256), 0, s, src, ix, st, dst, nout,
+                         sstride, dstride);
   } else {
-    launch_segsum<G>(s, src, ix, st, dst, nout);
+    launch_segsum<G>(s, src, ix, st, dst, nout, nmsm, sstride, dstride);
   }
 }
 
@@ -477,8 +481,10 @@ void WeightedReducer<G>::launch_tail_group(hipStream_t s, int set, int nmsm, boo
     Xyzz<F> *dst = last ? dense_buf_[set].as<Xyzz<F>>() : part_[set][l & 1].as<Xyzz<F>>();
     const uint32_t *ix = last ? idx_.as<uint32_t>() + final_perm_off_ : nullptr;
     const size_t sstride = (l & 1) ? maxp_ : maxp1_;  // level l - 1 wrote part_[(l - 1) & 1]
-    launch_segsum<G>(s, src, ix, starts_[l].as<uint32_t>(), dst, nout_[l], nmsm, sstride,
-                     last ? dense_slots() : (l & 1) ? maxp1_ : maxp_);
+    // coop (the batch's last group: nothing left to overlap): the narrow levels
+    // over 4 waves per add
+    launch_segsum_tail<G>(s, src, ix, starts_[l].as<uint32_t>(), dst, nout_[l], coop, nmsm, sstride,
+                          last ? dense_slots() : (l & 1) ? maxp1_ : maxp_);
     MSM_HIP_CHECK(hipGetLastError());
     src = dst;
   }

@@ -201,13 +201,17 @@ static __global__ void __launch_bounds__(256)
 
 // segment sums of <= 2 items (the reduction levels after level 0):
 // dst[t] = sum_{k in [starts[t], starts[t+1])} src[idx ? idx[k] : k]; longer
-// segments fold their leading items serially first
+// segments fold their leading items serially first.  grid.y: the MSMs of a
+// batch group (src / dst advanced by their strides, one plan for all)
 template <int G>
 static __global__ void __launch_bounds__(256)
     k_segsum_c(const Xyzz<typename FieldOf<G>::F> *__restrict__ src, const uint32_t *__restrict__ idx,
-               const uint32_t *__restrict__ starts, Xyzz<typename FieldOf<G>::F> *__restrict__ dst, size_t nout) {
+               const uint32_t *__restrict__ starts, Xyzz<typename FieldOf<G>::F> *__restrict__ dst, size_t nout,
+               size_t src_stride, size_t dst_stride) {
   typedef typename FieldOf<G>::F F;
   __shared__ CoopLds<F> L;
+  src += blockIdx.y * src_stride;
+  dst += blockIdx.y * dst_stride;
   const size_t t = (size_t)blockIdx.x * 64 + (threadIdx.x & 63);
   const bool active = t < nout;
   Xyzz<F> a = coop_inf<F>(), b = coop_inf<F>();
@@ -262,8 +266,11 @@ static __global__ void __launch_bounds__(256)
 // segment sums as k_segsum_c, for G2 on lane pairs
 static __global__ void __launch_bounds__(256)
     k_segsum_c2p(const Xyzz<Fp2> *__restrict__ src, const uint32_t *__restrict__ idx,
-                 const uint32_t *__restrict__ starts, Xyzz<Fp2> *__restrict__ dst, size_t nout) {
+                 const uint32_t *__restrict__ starts, Xyzz<Fp2> *__restrict__ dst, size_t nout, size_t src_stride,
+                 size_t dst_stride) {
   __shared__ CoopLds<Fp2L> L;
+  src += blockIdx.y * src_stride;
+  dst += blockIdx.y * dst_stride;
   const size_t t = (size_t)blockIdx.x * 32 + ((threadIdx.x & 63) >> 1);
   const bool active = t < nout;
   Xyzz<Fp2L> a = coop_inf2l(), b = coop_inf2l();
