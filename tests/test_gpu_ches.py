@@ -212,6 +212,38 @@ def test_mult_batch_sets_resident_and_pinned(m, group, log_n, K):
     ctx.close()
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("group,log_n,K", [(1, 12, 6), (2, 10, 4)])
+def test_mult_batch_waits_for_host_sets_written_on_its_stream(m, group, log_n, K):
+    """The batch's copy stream does not wait on the caller's stream (a copy
+    enqueued behind a cross-stream wait could block the host, ches.hip
+    run_jobs); the batch waits for the caller's prior work on the host instead.
+    Here the pinned host sets are produced by a D2H copy queued on the batch's
+    own stream behind ~20 ms of GPU spinning, and the batch is called without a
+    synchronise: it must see the new sets, not the zeros before them."""
+    import numpy as np
+    import torch
+    n = 1 << log_n
+    ctx = m.CHESContext(group, 0, n_exp=log_n)
+    ctx.build_table(m.fixed_points(group, n), n)
+    raw = np.concatenate([np.frombuffer(m.gen_scalars(n, 700 + k), dtype=np.uint8) for k in range(K)])
+    src = torch.tensor(raw, device="cuda:0")
+    want = [m.compress(group, ctx.mult(src.data_ptr() + k * n * 32, on_device=True)) for k in range(K)]
+    host = torch.zeros(K * n * 32, dtype=torch.uint8, pin_memory=True)
+    st = torch.cuda.Stream()
+    # a first host-set batch sizes the batch buffers (their first sizing
+    # synchronises the stream, which would hide a missing wait)
+    ctx.mult_batch(host.data_ptr(), K, set_stride=n * 32, on_device=False, stream=st.cuda_stream)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(st):
+        torch.cuda._sleep(50_000_000)
+        host.copy_(src, non_blocking=True)
+    got = ctx.mult_batch(host.data_ptr(), K, set_stride=n * 32, on_device=False, stream=st.cuda_stream)
+    torch.cuda.synchronize()
+    assert [m.compress(group, r) for r in got] == want
+    ctx.close()
+
+
 _FRONT_GROUP_SCRIPT = r"""
 import sys
 sys.path.insert(0, sys.argv[1])
