@@ -151,7 +151,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=20,
+                    help="untimed warm-up MSMs (default: one batch as long as the timed one)")
     ap.add_argument("--log-n", type=int, default=None,
                     help="weak scaling: 2^log_n points per GPU (default: strong scaling, 2^log_n_total / N per GPU)")
     ap.add_argument("--log-n-total", type=int, default=20, help="strong scaling: total points 2^log_n_total")

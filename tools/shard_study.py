@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--cfgs", default="22,20,19,18,16")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--warm", type=int, default=3, help="sets in the untimed warm-up batch")
+    ap.add_argument("--heat", type=int, default=0, help="bf16 GEMMs (8192^3) on the GPU right before the timed batches")
     ap.add_argument("--all", action="store_true", help="also print every repetition's ms per MSM")
     a = ap.parse_args()
     import numpy as np
@@ -54,6 +55,12 @@ def main():
             torch.cuda.synchronize(dev)
             setup = time.time() - t
             ctx.mult_batch(host.data_ptr(), min(a.warm, K), 32, set_stride=n * 32, on_device=False, stream=sp)
+            if a.heat:  # GPU busy without touching the MSM's data: clocks / power state, not caches
+                x = torch.randn(8192, 8192, device=dev, dtype=torch.bfloat16)
+                for _ in range(a.heat):
+                    x = (x @ x).clamp_(-1, 1)
+                torch.cuda.synchronize(dev)
+                del x
             res, every = {}, {}
             for mode, ptr, on_dev in (("resident", d.data_ptr(), True), ("h2d", host.data_ptr(), False)):
                 best = None
