@@ -976,13 +976,33 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
   // one pinned read-back slot per MSM of the batch: the host never waits inside
   // the issue loop, so MSM k+1's front is queued while MSM k still accumulates
   const size_t ob = red.out_bytes();  // a group's read-back lands contiguously
-  // reduction groups of R <= kGroup MSMs (balanced sizes), alternating between
-  // the two reducer sets / tail streams
+  // reduction groups of <= kGroup MSMs (balanced sizes), alternating between
+  // the reducer sets / tail streams.  MSM_LAST_GROUP=m (A/B knob): the batch's
+  // last m MSMs form a group of their own, so the earlier group's tail runs
+  // beside the last accumulations and only a narrow tail follows the last one
   static const size_t group_max = [] {  // A/B knob: MSMs per reduction group (default kGroup)
     const char *e = getenv("MSM_RED_GROUP");
     return (size_t)(e ? std::max(1, std::min(32, atoi(e))) : kGroup);
   }();
-  const size_t ngroups = (count + group_max - 1) / group_max, R = (count + ngroups - 1) / ngroups;
+  static const size_t last_env = [] {
+    const char *e = getenv("MSM_LAST_GROUP");
+    return (size_t)(e ? std::max(0, std::min(32, atoi(e))) : 0);
+  }();
+  std::vector<size_t> gfirst;  // group q holds MSMs [gfirst[q], gfirst[q + 1])
+  {
+    const size_t last = last_env && count > last_env ? std::min(last_env, group_max) : 0, nmain = count - last;
+    const size_t ng = (nmain + group_max - 1) / group_max, Rm = (nmain + ng - 1) / ng;
+    for (size_t k = 0; k < nmain; k += Rm) gfirst.push_back(k);
+    if (last) gfirst.push_back(nmain);
+    gfirst.push_back(count);
+  }
+  const size_t ngroups = gfirst.size() - 1;
+  std::vector<uint32_t> gof(count);
+  for (size_t q = 0; q < ngroups; ++q)
+    for (size_t k = gfirst[q]; k < gfirst[q + 1]; ++k) gof[k] = (uint32_t)q;
+  auto grp = [&](size_t k) { return (size_t)gof[k]; };              // the reduction group of MSM k
+  auto gslot = [&](size_t k) { return k - gfirst[gof[k]]; };        // its slot in the group
+  auto gend = [&](size_t k) { return k + 1 == gfirst[gof[k] + 1]; };  // the group's last MSM
   if (host_out_bytes_ < count * ob) {  // at least 256 MSMs' worth (a few hundred KiB): no regrowth per batch size
     if (host_out_) (void)hipHostFree(host_out_);
     host_out_ = nullptr;
@@ -1266,16 +1286,16 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
       }
       for (size_t k = k0; k < k1; ++k) MSM_HIP_CHECK(hipEventRecord(eva[k], L));
       for (size_t a = k0; a < k1;) {  // level 0, one launch per reduction group touched
-        const size_t q = a / R, b = std::min(k1, (q + 1) * R);
+        const size_t q = grp(a), b = std::min(k1, gfirst[q + 1]);
         if (q >= (size_t)nred) MSM_HIP_CHECK(hipStreamWaitEvent(L, evt[q - nred], 0));  // reducer set free again
         red.launch_head_slots(L, gbuckets_[gb].as<uint8_t>() + (a - k0) * NB * sizeof(Xyzz<typename FieldOf<G>::F>), NB,
-                              (int)(q % nred), (int)(a % R), (int)(b - a));
+                              (int)(q % nred), (int)gslot(a), (int)(b - a));
         a = b;
       }
       for (size_t k = k0; k < k1; ++k) MSM_HIP_CHECK(hipEventRecord(evh[k], L));
       for (size_t k = k0; k < k1; ++k) {  // tails of the reduction groups ending in [k0, k1)
-        if ((k + 1) % R != 0 && k + 1 != count) continue;
-        const size_t q = k / R, first = q * R;
+        if (!gend(k)) continue;
+        const size_t q = grp(k), first = gfirst[q];
         MSM_HIP_CHECK(hipStreamWaitEvent(ts, evh[k], 0));  // this lane's level 0s of group q
         if (k0 >= 1 && k0 - 1 >= first) MSM_HIP_CHECK(hipStreamWaitEvent(ts, evh[k0 - 1], 0));  // the other lane's
         red.launch_tail_group(ts, (int)(q % nred), (int)(k - first + 1), tail_coop && k + 1 == count);
@@ -1291,8 +1311,8 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
       copy_group(g + nsg);
       for (size_t k = fgb[g]; k < fgb[g + 1]; ++k) {
         hipStream_t L = lane[k % nl];
-        const size_t q = k / R;
-        const int bset = (int)(k % nl), slot = (int)(k % R), gset = (int)(q % nred);
+        const size_t q = grp(k);
+        const int bset = (int)(k % nl), slot = (int)gslot(k), gset = (int)(q % nred);
         MSM_HIP_CHECK(hipStreamWaitEvent(L, evf[g], 0));
         if (q >= (size_t)nred && slot < nl)  // reducer set q % nred free again
           MSM_HIP_CHECK(hipStreamWaitEvent(L, evt[q - nred], 0));
@@ -1305,7 +1325,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
         MSM_HIP_CHECK(hipEventRecord(eva[k], L));
         red.launch_head_slot(L, buckets_[bset].p, gset, slot);
         MSM_HIP_CHECK(hipEventRecord(evh[k], L));
-        if ((size_t)slot + 1 == R || k + 1 == count) {  // the group's level 0s are done on both lanes
+        if (gend(k)) {  // the group's level 0s are done on both lanes
           for (int d = 0; d < nl && d <= slot; ++d) MSM_HIP_CHECK(hipStreamWaitEvent(ts, evh[k - d], 0));
           red.launch_tail_group(ts, gset, slot + 1, tail_coop && k + 1 == count);
           red.copy_out_group(ts, gset, slot + 1, out_base + (k - slot) * ob);
@@ -1328,8 +1348,8 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
   }();
   const int fuse = nl < 2 ? fuse_env : 0;
   auto l0_group_tail = [&](size_t p) {  // after level 0 of MSM p (recorded as evh[p] on s)
-    const size_t pq = p / R, pslot = p % R;
-    if (pslot + 1 != R && p + 1 != count) return;
+    const size_t pq = grp(p), pslot = gslot(p);
+    if (!gend(p)) return;
     hipStream_t ts = tails_[pq % 2];
     MSM_HIP_CHECK(hipStreamWaitEvent(ts, evh[p], 0));
     red.launch_tail_group(ts, (int)(pq % 2), (int)pslot + 1, tail_coop && p + 1 == count);
@@ -1337,8 +1357,8 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
     MSM_HIP_CHECK(hipEventRecord(evt[pq], ts));
   };
   auto l0_set_free = [&](size_t p) {  // level 0 of MSM p may write its reducer set
-    const size_t pq = p / R;
-    if (p % R == 0 && pq >= 2) MSM_HIP_CHECK(hipStreamWaitEvent(s, evt[pq - 2], 0));
+    const size_t pq = grp(p);
+    if (gslot(p) == 0 && pq >= 2) MSM_HIP_CHECK(hipStreamWaitEvent(s, evt[pq - 2], 0));
   };
   for (size_t g = 0; g < (nl >= 2 || !fuse ? 0 : nfg); ++g) {
     copy_group(g + nsg);
@@ -1349,7 +1369,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
       if (prof) MSM_HIP_CHECK(hipEventRecord(acc_ev_[2 * k], s));
       if (k >= 1)
         accumulate_l0(s, (int)(g % nfr), (int)(k - fgb[g]), bset, job_table(k), (int)((k - 1) % kBSets),
-                      (int)(((k - 1) / R) % 2), (int)((k - 1) % R), fuse == 2);
+                      (int)(grp(k - 1) % 2), (int)gslot(k - 1), fuse == 2);
       else
         accumulate(s, (int)(g % nfr), (int)(k - fgb[g]), bset, job_table(k));
       if (prof) {
@@ -1367,7 +1387,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
   if (fuse && nl < 2) {  // level 0 of the last MSM, alone
     const size_t p = count - 1;
     l0_set_free(p);
-    red.launch_head_slot(s, buckets_[p % kBSets].p, (int)((p / R) % 2), (int)(p % R));
+    red.launch_head_slot(s, buckets_[p % kBSets].p, (int)(grp(p) % 2), (int)gslot(p));
     MSM_HIP_CHECK(hipEventRecord(evh[p], s));
     l0_group_tail(p);
   }
@@ -1375,7 +1395,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
     copy_group(g + nsg);
     MSM_HIP_CHECK(hipStreamWaitEvent(s, evf[g], 0));
     for (size_t k = fgb[g]; k < fgb[g + 1]; ++k) {
-      const int bset = (int)(k % kBSets), slot = (int)(k % R), gset = (int)((k / R) % 2);
+      const int bset = (int)(k % kBSets), slot = (int)gslot(k), gset = (int)(grp(k) % 2);
       hipStream_t ts = tails_[gset];
       if (k >= (size_t)kBSets) MSM_HIP_CHECK(hipStreamWaitEvent(s, evh[k - kBSets], 0));  // bucket set free again
       if (l0_first && k >= 1) MSM_HIP_CHECK(hipStreamWaitEvent(s, evh[k - 1], 0));
@@ -1389,7 +1409,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
       MSM_HIP_CHECK(hipStreamWaitEvent(ts, eva[k], 0));
       red.launch_head_slot(ts, buckets_[bset].p, gset, slot);
       MSM_HIP_CHECK(hipEventRecord(evh[k], ts));
-      if ((size_t)slot + 1 == R || k + 1 == count) {  // the reduction group's last MSM
+      if (gend(k)) {  // the reduction group's last MSM
         red.launch_tail_group(ts, gset, slot + 1, tail_coop && k + 1 == count);
         red.copy_out_group(ts, gset, slot + 1, out_base + (k - slot) * ob);
       }
