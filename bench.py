@@ -55,19 +55,24 @@ AFFINE_BYTES = 96              # one G1 affine point (blst layout), SURVEY 8d
 FPMUL_PER_MADD = 10            # 8M + 2S (ec_ops.h:727-748)
 MAD_RATE = 30.36e12            # measured chip v_mad_u64_u32 issue rate (lane-ops/s): profiles/r02_instr_rate.txt
 CPU_THREADS = 16               # the GPU box's CPU share per GPU (16 threads)
-DEFAULT_BETA = {}              # log_n -> ches_config_files variant used by default; _beta at 2^20 measured slower
+# (group, log_n) -> the ches_config_files variant used by default: G1 2^20 keeps config_file_n_exp_20.h
+# (_beta measured slower); G2 2^20 takes config_file_n_exp_20_beta.h (q = 2^20, h = 13), faster in
+# 3 of 3 alternating runs, 164-167 vs 159-165 M pairs/s (profiles/r05_g2_beta_ab.txt)
+DEFAULT_BETA = {(2, 20): 1}
 # CHES configuration per point count (n_exp, beta of a ches_config_files header; its q, h and a_h are valid
 # for any point count): the strong-scaling shards of `--gpus N` (2^20 / N points per rank) take the
 # configuration MEASURED fastest for that shard size on MI355X (tools/shard_study.py,
-# profiles/r05_shard_study.txt), not necessarily the reference's config_file_n_exp_<log2 shard>.h
+# profiles/r05_shard_pip_study.txt), not necessarily the reference's config_file_n_exp_<log2 shard>.h
 SHARD_CONFIG = {}
 
 
-def ches_config(log_n, beta=None):
+def ches_config(log_n, beta=None, group=1):
     """(n_exp, beta) of the CHES configuration for 2^log_n points per GPU."""
     if beta is not None:
         return log_n, beta
-    return SHARD_CONFIG.get(log_n, (log_n, DEFAULT_BETA.get(log_n, 0)))
+    if group == 1 and log_n in SHARD_CONFIG:
+        return SHARD_CONFIG[log_n]
+    return log_n, DEFAULT_BETA.get((group, log_n), 0)
 
 
 def isa_mads_per_madd(G=1, path=os.path.join(REPO, "profiles", "r04_isa_counts.txt")):
@@ -237,7 +242,7 @@ def main():
             return parts
         return [mdist.fold(ps, add) for ps in mdist.gather_partials_batch(parts, G, xdev)]
 
-    cfg_n, beta = ches_config(args.log_n, args.beta)  # the config file this point count uses (SHARD_CONFIG)
+    cfg_n, beta = ches_config(args.log_n, args.beta, G)  # the config file this point count uses (SHARD_CONFIG)
 
     def has_config(b):
         try:
@@ -632,12 +637,12 @@ def config_legs(m, torch, dev, local, sp, pts, host, K, W):
     # ---- configs[4]: G2 2^20 CHES batch ----
     t = time.time()
     pts2_host = m.fixed_points(2, n20)
-    c2 = m.CHESContext(2, local, n_exp=20)
+    c2 = m.CHESContext(2, local, n_exp=20, beta=ches_config(20, group=2)[1])
     c2.build_table(pts2_host, n20, stream=sp)
     c2.set_profiling(True)
     torch.cuda.synchronize(dev)
     setup = time.time() - t
-    k2 = min(K, 10)
+    k2 = K  # the headline's batch length
     hptr, SS = host.data_ptr(), 32 * n20
     d2 = host[:k2 * SS].to(dev)
     c2.mult_batch(hptr, min(max(W, 1), k2), 32, set_stride=SS, on_device=False, stream=sp)
