@@ -596,6 +596,18 @@ def config_legs(m, torch, dev, local, sp, pts, host, K, W):
         "parity_vs_reference": m.compress(1, r[0]).hex() == _golden(m, 1, n20),
         "note": "the drop-in boundary (pippenger_blst_built_in, main_p1.cpp:400-436): per call 96 MiB of points + "
                 "32 MiB of scalars from pageable host memory, digits/sort overlapping the point upload"}
+    # the same calls with the point array registered once (msm_register_host_table): no point upload
+    L = m.lib()
+    if L.msm_register_host_table(1, P20, n20) == 0:
+        for _ in range(2):
+            dropin(1, P20, sets20[0], n20)
+        r, el = timed(lambda k: dropin(1, P20, sets20[k], n20), k20)
+        L.msm_unregister_host_table(P20)
+        legs["blst_p1s_mult_pippenger_2^20_registered"] = {
+            "value": round(n20 * k20 / el, 1), "unit": "pairs/s", "ms_per_step": round(el / k20 * 1e3, 4),
+            "parity_vs_reference": m.compress(1, r[0]).hex() == _golden(m, 1, n20),
+            "note": "the same drop-in calls after msm_register_host_table(P, n) once: the points are read from "
+                    "their device copy, only the 32 MiB of scalars cross PCIe per call"}
     del sets20, P20
 
     # ---- configs[0]: CPU reference at 2^10, and the drop-in at the same size ----

@@ -212,7 +212,12 @@ size_t msm_set_engine_cache_limit(size_t bytes);
  * tile call (blst_p{1,2}_tile_pippenger_d_CHES, _noindexhash, _BGMW95) whose
  * pointers all lie on row boundaries inside one registered table sends 4-B row
  * indices instead of gathering and uploading every 96/192-B row (1.2 GB per
- * G1 2^20 call).  Any pointer outside the table falls back to the gather.  The
+ * G1 2^20 call).  Any pointer outside the table falls back to the gather.  A
+ * point array registered the same way serves the plain drop-in: a flat
+ * {ptr, NULL} blst_p{1,2}s_mult_pippenger / _tile_pippenger call whose npoints
+ * points lie inside one registered table reads their device copy instead of
+ * uploading 96/192 B per point (ref multi_scalar.c:549-607; callers that
+ * multiply one SRS many times).  The
  * caller must not modify or free the rows while they are registered (as with
  * hipHostRegister).  group 1 (G1, blst_p1_affine rows) or 2 (G2); registering
  * an already registered base replaces it.  Returns MSM_OK or an error code. */

@@ -110,6 +110,21 @@ const uint8_t *contiguous(std::vector<uint8_t> &buf, const void *const *ptrs, si
   return buf.data();
 }
 
+// The device rows of n points at `pts` when a registered host table holds all
+// of them (msm_register_host_table; table_registry.hpp), else nullptr.  `hold`
+// keeps the table alive for the call.
+template <int G>
+const void *registered_rows(const uint8_t *pts, size_t n, std::shared_ptr<HostTable> &hold) {
+  int dev = 0;
+  MSM_HIP_CHECK(hipGetDevice(&dev));
+  std::shared_ptr<HostTable> t = TableRegistry::get().find(G, dev, pts);
+  if (!t) return nullptr;
+  const size_t off = (size_t)(pts - t->base) / (96 * G);
+  if (off + n > t->nrows) return nullptr;
+  hold = t;
+  return t->rows.template as<uint8_t>() + off * t->row_bytes;
+}
+
 template <int G>
 void mult_pippenger(void *ret, const void *const *points, size_t n, const byte *const *scalars, size_t nbits) {
   typedef typename HostField<G>::F HF;
@@ -123,8 +138,10 @@ void mult_pippenger(void *ret, const void *const *points, size_t n, const byte *
   std::vector<uint8_t> pbuf, sbuf;
   const uint8_t *pts = contiguous(pbuf, points, n, 96 * G);
   const uint8_t *sc = contiguous(sbuf, (const void *const *)scalars, n, nb);
+  std::shared_ptr<HostTable> hold;
+  const void *rows = registered_rows<G>(pts, n, hold);  // points registered once: no upload
   auto eng = pippenger_engine<G>(auto_window(n));
-  (*eng)->run_host(eng->stream(), pts, n, sc, nb, (int)nbits, &out);
+  (*eng)->run_host(eng->stream(), pts, n, sc, nb, (int)nbits, &out, nullptr, rows);
   memcpy(ret, &out, sizeof out);
 }
 
@@ -156,8 +173,10 @@ void tile_pippenger(void *ret, const void *const *points, size_t n, const byte *
   std::vector<uint8_t> pbuf, sbuf;
   const uint8_t *pts = contiguous(pbuf, points, n, 96 * G);
   const uint8_t *sc = contiguous(sbuf, (const void *const *)scalars, n, nb);
+  std::shared_ptr<HostTable> hold;
+  const void *rows = registered_rows<G>(pts, n, hold);
   auto eng = pippenger_engine<G>(8);
-  (*eng)->run_host(eng->stream(), pts, n, sc, nb, (int)nbits, &out, &t);
+  (*eng)->run_host(eng->stream(), pts, n, sc, nb, (int)nbits, &out, &t, rows);
   memcpy(ret, &out, sizeof out);
 }
 

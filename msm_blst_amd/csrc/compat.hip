@@ -351,6 +351,7 @@ void register_host_table(const void *rows, size_t nrows) {
   t->group = G;
   t->base = static_cast<const uint8_t *>(rows);
   t->nrows = nrows;
+  t->row_bytes = sizeof(AffP<F>);
   t->rows.ensure(nrows * sizeof(AffP<F>));
   const size_t psz = 96 * G, chunk = std::min<size_t>(nrows, ((size_t)64 << 20) / psz);
   hipStream_t s;

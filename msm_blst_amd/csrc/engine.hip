@@ -202,8 +202,11 @@ void Pippenger<G>::accumulate(hipStream_t s, int nbits, ChesFrontSet &f, DevBuf 
   const int W = (nbits + 1 + c_ - 1) / c_;
   const size_t NT = (size_t)W << (c_ - 1);
   bk.ensure(NT * sizeof(Xyzz<F>));
-  launch_accumulate<G>(s, f.sort.sched(f.order.as<uint32_t>(), f.sorted.as<uint32_t>(), 0, NT), pts_.as<Aff<F>>(),
-                       bk.as<Xyzz<F>>(), NT);
+  const AccSched sched = f.sort.sched(f.order.as<uint32_t>(), f.sorted.as<uint32_t>(), 0, NT);
+  if (ext_rows_)
+    launch_accumulate<G>(s, sched, static_cast<const AffP<F> *>(ext_rows_), bk.as<Xyzz<F>>(), NT);
+  else
+    launch_accumulate<G>(s, sched, pts_.as<Aff<F>>(), bk.as<Xyzz<F>>(), NT);
   MSM_HIP_CHECK(hipGetLastError());
 }
 
@@ -454,7 +457,7 @@ void Pippenger<G>::run_batch(hipStream_t s, const uint8_t *d_scalars, size_t str
 // multiplies with |d| (cbits + 1 bits) and the signs.
 template <int G>
 void Pippenger<G>::run_host(hipStream_t s, const void *pts_blst, size_t n, const uint8_t *scalars, size_t stride,
-                            int nbits, hfp::Jac<HF> *out, const TileSpec *tile) {
+                            int nbits, hfp::Jac<HF> *out, const TileSpec *tile, const void *dev_rows) {
   typedef typename FieldOf<G>::F F;
   DeviceGuard g(dev_);
   if (nbits < 1 || nbits > 256) throw std::runtime_error("nbits must be in [1,256]");
@@ -490,6 +493,17 @@ void Pippenger<G>::run_host(hipStream_t s, const void *pts_blst, size_t n, const
     front(s, reinterpret_cast<const uint8_t *>(mag), 4, nbits, neg, fs_[0]);
   } else {
     front(s, scal_.as<uint8_t>(), stride, nbits, nullptr, fs_[0]);
+  }
+  if (dev_rows) {  // registered points: resident already, nothing to upload
+    ext_rows_ = dev_rows;
+    try {
+      back(s, nbits, out);
+    } catch (...) {
+      ext_rows_ = nullptr;
+      throw;
+    }
+    ext_rows_ = nullptr;
+    return;
   }
   const size_t raw = n * 96 * G;
   tmp_.ensure(raw);

@@ -289,14 +289,17 @@ class Pippenger {
   // points (blst affine) and scalars in host memory: set_points + run with the
   // point upload overlapping the scalars' digits and sort (blst drop-in)
   // tile: one blst window tile instead of the whole MSM (blst_p{1,2}s_tile_pippenger)
+  // dev_rows: the points already on this device as AffP rows (a registered
+  // host table holding them, table_registry.hpp): nothing is uploaded
   void run_host(hipStream_t s, const void *points_blst, size_t n, const uint8_t *scalars, size_t stride, int nbits,
-                hfp::Jac<HF> *out, const TileSpec *tile = nullptr);
+                hfp::Jac<HF> *out, const TileSpec *tile = nullptr, const void *dev_rows = nullptr);
   // `count` MSMs over the resident points, scalar set k at d_scalars + k
-  // set_stride (device memory), pipelined: front k + 2 (digits + sort) on a
-  // front stream beside accumulation k; accumulations alternate between two
-  // lane streams (each followed by its level 0); the reduction tails of groups
-  // of <= 8 MSMs on a tail stream; the host Horner of group q overlaps the GPU
-  // work of later groups.  Results equal `count` run() calls.
+  // set_stride (device memory), pipelined: fronts in groups of up to 4 sets (one
+  // digits + sort pass per stage) on a front stream, each group's accumulations
+  // in one launch on one of two alternating lane streams (followed by its level
+  // 0s); the reduction tails of groups of <= 8 MSMs on a tail stream; the host
+  // Horner of group q overlaps the GPU work of later groups.  Results equal
+  // `count` run() calls.
   void run_batch(hipStream_t s, const uint8_t *d_scalars, size_t stride, size_t set_stride, size_t count, int nbits,
                  hfp::Jac<HF> *outs);
   size_t npoints() const { return n_; }
@@ -321,6 +324,7 @@ class Pippenger {
   DevBuf pts_, buckets_[2], tmp_, scal_;
   std::unique_ptr<HostStager> stage_;  // run_host: uploads from the caller's pageable memory
   hipStream_t up_ = nullptr;  // run_host: point upload stream
+  const void *ext_rows_ = nullptr;  // run_host with dev_rows: the accumulation reads AffP rows from there
   hipEvent_t ev_up_ = nullptr, ev_s_ = nullptr;
   // run_batch: front stream, second accumulation lane, tail stream; events; read-back slots
   // run_batch streams: fronts, lane 1 (lane 0 is the caller's), tails

@@ -7,7 +7,8 @@
 // lives on its device in the engine's row layout (AffP: one 128-B line per G1
 // row); a tile whose pointers all hit row boundaries of one registered table
 // then ships 4-B row indices instead of gathering 96/192-B rows on the host
-// (compat.hip entry_msm_ptrs).  Process-wide, thread-safe; a call holds a
+// (compat.hip entry_msm_ptrs); a flat point array inside one feeds the plain
+// drop-in and its tiles without an upload (abi.cpp).  Process-wide, thread-safe; a call holds a
 // shared_ptr to the table it uses, so unregistering during a call is safe.
 #pragma once
 #include <stdint.h>
@@ -25,6 +26,7 @@ struct HostTable {
   const uint8_t *base = nullptr;  // caller's rows (blst affine, 96 G bytes each)
   size_t nrows = 0;
   DevBuf rows;  // AffP<F> rows on `device`
+  size_t row_bytes = 0;  // sizeof(AffP<F>)
 };
 
 class TableRegistry {
