@@ -1203,9 +1203,28 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
     const char *e = getenv("MSM_FRONT_AFTER_L0");
     return e && atoi(e) != 0;
   }();
+  // Paced copies (MSM_COPY_PACE=L, default 8; 0 or < 3: all at the batch
+  // start): the first L front groups' sets are copied at the batch start, the
+  // copy of group g >= L is issued when the accumulation L MSMs before it has
+  // finished (a host wait on its event -- no cross-stream wait on the copy
+  // stream), so later copies run one per period beside one MSM instead of back
+  // to back beside the first five: 2^20 H2D 436.4 / 439.2 / 439.9 vs 432.4 /
+  // 436.2 / 436.7 M pairs/s (L = 8 vs all at the start, tools/h2d_ab.py
+  // medians, alternating on one box; profiles/r05_copy_pace_ab.txt).  The wait
+  // only ever targets work already enqueued (or an event of an earlier batch,
+  // which has completed), so it cannot deadlock; the host stays L MSMs ahead.
+  static const size_t pace_env = [] {
+    const char *e = getenv("MSM_COPY_PACE");
+    return (size_t)(e ? std::max(0, std::min(32, atoi(e))) : 8);
+  }();
+  const size_t pace = scalars_on_host && !zero_copy && pace_env >= 3 ? pace_env : 0;
   auto front_group = [&](size_t g) {
     if (g >= nfg) return;
     const bool copied = scalars_on_host && !zero_copy;
+    if (pace && g >= pace && g < nsg) {
+      MSM_HIP_CHECK(hipEventSynchronize(eva[fgb[g] - pace]));
+      copy_group(g);
+    }
     if (copied) MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, evc[g], 0));
     if (g >= (size_t)nfr) {  // front set g % nfr: every accumulation of group g - nfr has read it
       const size_t last = fgb[g - nfr + 1] - 1;
@@ -1222,7 +1241,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
                 fine_bt);
     MSM_HIP_CHECK(hipEventRecord(evf[g], fstream_));
   };
-  for (size_t g = 0; g < nsg; ++g) copy_group(g);
+  for (size_t g = 0; g < (pace ? std::min(nsg, pace) : nsg); ++g) copy_group(g);
   // Accumulation k waits for level 0 of MSM k - 1, so level 0 runs beside the
   // fronts, never beside the next accumulation.  Without this wait the batch
   // fell, in about one run in three, into a schedule where fronts ran two MSMs
