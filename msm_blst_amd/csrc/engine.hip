@@ -434,11 +434,14 @@ void Pippenger<G>::run_batch(hipStream_t s, const uint8_t *d_scalars, size_t str
     }
     issue_fronts(g + nfr - 1);
   }
-  // the host Horner of group q overlaps the GPU work of later groups
+  // the host Horner of group q (one per MSM, ~W c doublings each) overlaps the
+  // GPU work of later groups, spread over the host worker threads
   for (size_t q = 0; q * R < count; ++q) {
     MSM_HIP_CHECK(hipEventSynchronize(evt[q]));
-    for (size_t k = q * R; k < std::min(count, (q + 1) * R); ++k)
-      outs[k] = red.combine_windows((const uint8_t *)host_out_ + k * ob, c_);
+    const size_t k0 = q * R, k1 = std::min(count, (q + 1) * R);
+    WorkerPool::get().parallel_for(k1 - k0, [&](size_t i) {
+      outs[k0 + i] = red.combine_windows((const uint8_t *)host_out_ + (k0 + i) * ob, c_);
+    });
   }
   // the caller's stream observes completion of every stream of the batch
   for (hipStream_t q : {fstream_, lane1_, tstream_}) {

@@ -297,7 +297,7 @@ class Pippenger {
   // set_stride (device memory), pipelined: fronts in groups of up to 4 sets (one
   // digits + sort pass per stage) on a front stream, each group's accumulations
   // in one launch on one of two alternating lane streams (followed by its level
-  // 0s); the reduction tails of groups of <= 8 MSMs on a tail stream; the host
+  // 0s); the reduction tails of groups of <= 10 MSMs on a tail stream; the host
   // Horner of group q overlaps the GPU work of later groups.  Results equal
   // `count` run() calls.
   void run_batch(hipStream_t s, const uint8_t *d_scalars, size_t stride, size_t set_stride, size_t count, int nbits,
@@ -316,7 +316,10 @@ class Pippenger {
   size_t n_ = 0;
   bool profile_ = false;
   PhaseTimes times_;
-  static constexpr int kFronts = 5, kGroup = 8, kRedSets = 4;
+  // kGroup: MSMs per reduction group; 10 (two tails for the 20-MSM configs[1]
+  // batch) since the host Horner of a group runs on the worker threads: 0.327-
+  // 0.339 vs 0.341-0.353 ms per 2^16 MSM with 8 (profiles/r05_pip_group_ab.txt)
+  static constexpr int kFronts = 5, kGroup = 10, kRedSets = 4;
   // digit/sort outputs: fs_[0] for run(); run_batch rotates kFronts of them, or
   // with the front phase one per front group (up to kFrontPhase)
   std::vector<ChesFrontSet> fs_ = std::vector<ChesFrontSet>(kFronts);

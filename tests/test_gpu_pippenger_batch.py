@@ -5,7 +5,7 @@ stream) the reference's golden value (tests/golden, written from the
 reference's own blst_p1s_mult_pippenger).  Covers device and host scalar
 sets, G1 and G2, window sizes with a partial top window (bucket copies),
 64-bit scalars (short window plan) and batch lengths that are not a multiple
-of the plain-Pippenger reduction group (Pippenger::kGroup = 8,
+of the plain-Pippenger reduction group (Pippenger::kGroup = 10,
 engine.hpp; the CHES batch groups 20)."""
 import numpy as np
 import pytest
@@ -32,7 +32,8 @@ def _sets(m, n, k):
 
 @pytest.mark.parametrize("group,lg,c,count,on_device", [
     (1, 16, 14, 10, True),   # configs[1]: 2^16, the drop-in's window
-    (1, 16, 13, 17, False),  # blst's window for 2^16; host sets; 3 groups (6/6/5)
+    (1, 16, 13, 17, False),  # blst's window for 2^16; host sets; 2 groups (9/8)
+    (1, 12, 12, 23, True),   # 3 reduction groups (8/8/7), two front-group ramps
     (1, 10, 10, 3, True),
     (2, 10, 10, 9, True),
 ])
