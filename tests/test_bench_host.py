@@ -34,3 +34,26 @@ def test_mads_per_madd_without_counts(tmp_path):
     missing = str(tmp_path / "none.txt")
     assert bench.isa_mads_per_madd(1, missing)[0] == 3567  # the round-3 constant
     assert bench.isa_mads_per_madd(2, missing)[0] is None  # no G2 figure without lane-pair counts
+
+
+def test_ches_config_per_group_and_shard_size():
+    """The configuration each bench line uses: G1 2^20 the reference's
+    config_file_n_exp_20.h, G2 2^20 its _beta variant (measured faster for G2,
+    profiles/r05_g2_beta_ab.txt), the strong-scaling shards the reference's
+    file for their own point count, and an explicit --beta wins."""
+    assert bench.ches_config(20) == (20, 0)
+    assert bench.ches_config(20, group=2) == (20, 1)
+    for lg in (17, 18, 19):
+        assert bench.ches_config(lg) == (lg, 0)
+    assert bench.ches_config(20, 0, 2) == (20, 0)
+    assert bench.ches_config(20, 1, 1) == (20, 1)
+
+
+def test_default_warmup_is_one_batch():
+    """bench.py's default warm-up is one untimed batch as long as the timed one
+    (the first short-warm-up batch runs below steady-state clocks,
+    profiles/r05_warmup_ab.txt)."""
+    src = open(os.path.join(REPO, "bench.py")).read()
+    steps = int(re.search(r'"--steps", type=int, default=(\d+)', src).group(1))
+    warm = int(re.search(r'"--warmup", type=int, default=(\d+)', src).group(1))
+    assert warm == steps == 20
