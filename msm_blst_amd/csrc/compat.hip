@@ -331,10 +331,11 @@ void entry_msm_ptrs(void *ret, const void *const *points, size_t ne, EntryFill f
     MSM_HIP_CHECK(hipMemcpyAsync(S.xfer.template as<uint8_t>() + c0 * psz, slot, cnt * psz, hipMemcpyHostToDevice, S.up));
     MSM_HIP_CHECK(hipEventRecord(S.ring_ev[k], S.up));
     used[k] = true;
+    // convert this chunk while the next one is gathered and copied
+    hipLaunchKernelGGL(k_convert_points<G>, dim3(nblk(cnt, 256)), dim3(256), 0, S.up,
+                       S.xfer.template as<uint64_t>() + c0 * (psz / 8), S.pts.template as<Aff<F>>() + c0, cnt);
+    MSM_HIP_CHECK(hipGetLastError());
   }
-  hipLaunchKernelGGL(k_convert_points<G>, dim3(nblk(ne, 256)), dim3(256), 0, S.up, S.xfer.template as<uint64_t>(),
-                     S.pts.template as<Aff<F>>(), ne);
-  MSM_HIP_CHECK(hipGetLastError());
   MSM_HIP_CHECK(hipEventRecord(S.up_ev, S.up));
   MSM_HIP_CHECK(hipStreamWaitEvent(s, S.up_ev, 0));
   clk.lap("gather");
