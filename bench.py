@@ -55,6 +55,7 @@ AFFINE_BYTES = 96              # one G1 affine point (blst layout), SURVEY 8d
 FPMUL_PER_MADD = 10            # 8M + 2S (ec_ops.h:727-748)
 MAD_RATE = 30.36e12            # measured chip v_mad_u64_u32 issue rate (lane-ops/s): profiles/r02_instr_rate.txt
 CPU_THREADS = 16               # the GPU box's CPU share per GPU (16 threads)
+CPU_SETS = 3                   # scalar sets in the 1-thread CPU sample (~12 s at 2^20)
 # (group, log_n) -> the ches_config_files variant used by default: G1 2^20 keeps config_file_n_exp_20.h
 # (_beta measured slower); G2 2^20 takes config_file_n_exp_20_beta.h (q = 2^20, h = 13), faster in
 # 3 of 3 alternating runs, 164-167 vs 159-165 M pairs/s (profiles/r05_g2_beta_ab.txt)
@@ -1006,13 +1007,19 @@ def cpu_baseline(m, pts, host, n, K, gpu_res, G, log_n):
         mult.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
         scratch = (ctypes.c_uint8 * sizeof(k))()
         pp = (ctypes.c_void_p * 2)(ctypes.cast(P, ctypes.c_void_p), None)
-        sp = (ctypes.c_void_p * 2)(ctypes.cast(S0, ctypes.c_void_p), None)
-        r = (ctypes.c_uint8 * (144 * G))()
-        t = time.perf_counter()
-        mult(r, pp, k, sp, 255, scratch)
-        dt1 = time.perf_counter() - t
-        one = {"value": round(k / dt1, 1), "cores": 1, "seconds": round(dt1, 2),
-               "matches_gpu": (m.compress(G, bytes(r)) == m.compress(G, gpu_res[0])) if full else None}
+        # a bounded sample of ~10-15 s: the first CPU_SETS scalar sets, each checked against the GPU
+        nsets = min(CPU_SETS, K)
+        dt1, match = 0.0, True
+        for j in range(nsets):
+            Sj = S0 if j == 0 else (ctypes.c_uint8 * (32 * k)).from_buffer_copy(sc[j * n * 32:j * n * 32 + 32 * k].tobytes())
+            sp = (ctypes.c_void_p * 2)(ctypes.cast(Sj, ctypes.c_void_p), None)
+            r = (ctypes.c_uint8 * (144 * G))()
+            t = time.perf_counter()
+            mult(r, pp, k, sp, 255, scratch)
+            dt1 += time.perf_counter() - t
+            match = match and m.compress(G, bytes(r)) == m.compress(G, gpu_res[j])
+        one = {"value": round(nsets * k / dt1, 1), "cores": 1, "seconds": round(dt1, 2), "sets": nsets,
+               "matches_gpu": match if full else None}
         kind = "reference"
         Gd = _ref_lib("libref_grid.so")
         if Gd is not None:
@@ -1030,7 +1037,7 @@ def cpu_baseline(m, pts, host, n, K, gpu_res, G, log_n):
             multi = None
         out = {"value": one["value"], "unit": "pairs/s", "cores": 1, "kind": kind,
                "sample": f"reference libblst blst_p{G}s_mult_pippenger (oracle/_ref), 1 thread, "
-                         f"first 2^{log_n} points, scalar set 0, {dt1:.1f}s",
+                         f"first 2^{log_n} points, scalar sets 0-{one['sets'] - 1}, {dt1:.1f}s",
                "matches_gpu": one["matches_gpu"], "all_cores": multi}
     else:
         sys.path.insert(0, os.path.join(REPO, "tests"))
