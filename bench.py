@@ -50,10 +50,12 @@ METRIC = "G1 MSM point-scalar pairs/sec at n=2^20, 1/2/4/8 MI355X; bit-exact vs 
 METRIC_G2 = "G2 MSM point-scalar pairs/sec at n=2^20 (BASELINE configs[4]); bit-exact vs CPU"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 MADS_PER_FPMUL = 392           # 14x14 product + 14x14 reduction, one v_mad_u64_u32 each (fp.hpp)
-FPMUL_PEAK = 76.8e9            # measured register-resident Fp-mul/s: profiles/r02_fp_rate.txt (tools/microbench/fp_rate.hip)
+FPMUL_PEAK = 76.8e9            # round-2 register-resident Fp-mul/s (profiles/r02_fp_rate.txt): fallback only, the
+                               # line prices against msm_valu_probe's rates measured in the same run
+MADD_RATE_R02 = 7.32e9         # round-2 register-resident G1 xyzz madd/s: fallback only
 AFFINE_BYTES = 96              # one G1 affine point (blst layout), SURVEY 8d
 FPMUL_PER_MADD = 10            # 8M + 2S (ec_ops.h:727-748)
-MAD_RATE = 30.36e12            # measured chip v_mad_u64_u32 issue rate (lane-ops/s): profiles/r02_instr_rate.txt
+MAD_RATE = 30.36e12            # round-2 chip v_mad_u64_u32 rate (profiles/r02_instr_rate.txt): fallback only
 CPU_THREADS = 16               # the GPU box's CPU share per GPU (16 threads)
 CPU_SETS = 3                   # scalar sets in the 1-thread CPU sample (~12 s at 2^20)
 # (group, log_n) -> the ches_config_files variant used by default: G1 2^20 keeps config_file_n_exp_20.h
@@ -96,6 +98,30 @@ def isa_mads_per_madd(G=1, path=os.path.join(REPO, "profiles", "r04_isa_counts.t
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def leg(value, ms, ok=None, **kw):
+    """One leg of the JSON line in its compact form (round 6: the whole line
+    must fit the driver's record): M = M pairs/s, ms = ms per MSM, ok = parity
+    (bit-exact vs the reference's golden result); the leg names and extra keys
+    are documented in DESIGN.md sec.13."""
+    d = {"M": None if value is None else round(value / 1e6, 2), "ms": None if ms is None else round(ms, 4)}
+    if ok is not None:
+        d["ok"] = ok
+    d.update(kw)
+    return d
+
+
+def valu_probe(m, device):
+    """The device's VALU ceilings measured now (msm_valu_probe, csrc/probe.hip):
+    v_mad_u64_u32 lane-ops/s, Fp-mul/s and register-resident G1 madd/s; None
+    when the library lacks the probe."""
+    out = (ctypes.c_double * 4)()
+    try:
+        rc = m.lib().msm_valu_probe(device, out)
+    except AttributeError:
+        return None
+    return {"mad": out[0], "fpmul": out[1], "madd": out[2], "ms": out[3]} if rc == 0 else None
 
 
 class Bracket:
@@ -301,35 +327,25 @@ def main():
             parts = ctx.mult_batch(hptr, K, 32, set_stride=SS, on_device=False, stream=sp)
             res = fold_all(parts)
         elapsed, acc_ms = b.elapsed, ctx.phase_times()["accumulate"]
-        legs["ches_batch_h2d"] = {"value": round(n * world * K / elapsed, 1), "ms_per_step": round(elapsed / K * 1e3, 4),
-                                  "kernel_ms": round(acc_ms, 4),
-                                  "note": "headline: K distinct scalar sets in pinned host memory, H2D in the timed region"}
+        legs["ches_h2d"] = leg(n * world * K / elapsed, elapsed / K * 1e3, kernel_ms=round(acc_ms, 4))
         if not args.no_compare:
             with Bracket(world, dev, xdev) as b:
                 rparts = fold_all(ctx.mult_batch(dptr, K, 32, set_stride=SS, on_device=True, stream=sp))
-            legs["ches_batch_resident"] = {"value": round(n * world * K / b.elapsed, 1),
-                                           "ms_per_step": round(b.elapsed / K * 1e3, 4),
-                                           "kernel_ms": round(ctx.phase_times()["accumulate"], 4),
-                                           "equals_h2d_batch": keys(rparts) == keys(res),
-                                           "note": "the same K sets already resident in HBM (kernel-only rate)"}
+            legs["ches_res"] = leg(n * world * K / b.elapsed, b.elapsed / K * 1e3, keys(rparts) == keys(res),
+                                   kernel_ms=round(ctx.phase_times()["accumulate"], 4))
             if world == 1 and has_config(1 - beta):  # the reference's other configuration for this n
                 octx, _ = make("ches", 1 - beta)
                 octx.mult_batch(dptr, min(max(W, 1), K), 32, set_stride=SS, on_device=True, stream=sp)
                 with Bracket(world, dev, xdev) as b:
                     oparts = octx.mult_batch(dptr, K, 32, set_stride=SS, on_device=True, stream=sp)
                 op = octx.params
-                legs[f"ches_batch_resident_beta{1 - beta}"] = {
-                    "value": round(n * K / b.elapsed, 1), "ms_per_step": round(b.elapsed / K * 1e3, 4),
-                    "kernel_ms": round(octx.phase_times()["accumulate"], 4),
-                    "equals_h2d_batch": keys(oparts) == keys(res),
-                    "note": f"the reference's other n=2^{args.log_n} configuration "
-                            f"(config_file_n_exp_{cfg_n}{'_beta' if beta == 0 else ''}.h: q=2^{op['q_exp']}, "
-                            f"h={op['h']}, |B|={op['b_size']}), same K resident sets"}
+                legs[f"ches_res_beta{1 - beta}"] = leg(n * K / b.elapsed, b.elapsed / K * 1e3, keys(oparts) == keys(res),
+                                                       kernel_ms=round(octx.phase_times()["accumulate"], 4),
+                                                       cfg=f"q{op['q_exp']}h{op['h']}")
                 octx.close()
             sres, sel = sync_steps(mult, K, True)
-            legs["ches_sync"] = {"value": round(n * world * K / sel, 1), "ms_per_step": round(sel / K * 1e3, 4),
-                                 "note": "K synchronous msm_ches_ctx_mult calls on resident sets (per-MSM latency)"}
             batch_eq_sync = keys(sres) == keys(res)
+            legs["ches_sync"] = leg(n * world * K / sel, sel / K * 1e3, batch_eq_sync)
         else:
             batch_eq_sync = None
         mult(0)  # one profiled synchronous MSM for the phase split
@@ -341,8 +357,7 @@ def main():
         phases = ctx.phase_times()
         acc_ms = phases["accumulate"]
         batch_eq_sync = None
-        legs[args.method + "_sync_h2d"] = {"value": round(n * world * K / elapsed, 1),
-                                           "ms_per_step": round(elapsed / K * 1e3, 4)}
+        legs[args.method + "_sync_h2d"] = leg(n * world * K / elapsed, elapsed / K * 1e3)
 
     # ---- parity ----
     gold = json.load(open(os.path.join(REPO, "tests", "golden", f"msm_g{G}.json")))
@@ -358,6 +373,13 @@ def main():
         cross = all_true(m.compress(G, pp) == m.compress(G, mine), world, xdev)
         pctx.close()
 
+    # the device's VALU ceilings, measured now (after the timed region, GPU warm):
+    # twice, keeping the higher rate (the first call also warms the probe kernels)
+    probe = None
+    for _ in range(2):
+        p = valu_probe(m, local)
+        if p is not None:
+            probe = p if probe is None else {k: max(probe[k], p[k]) for k in p}
     others = {}
     if world == 1 and not args.no_compare:  # the reference's other methods, same points, resident sets
         for ometh in ("ches", "pippenger", "bgmw"):
@@ -368,17 +390,15 @@ def main():
             for _ in range(2):
                 omult(0)
             ores, oel = sync_steps(omult, k, True)
-            others[ometh] = {"value": round(n * k / oel, 1), "unit": "pairs/s",
-                             "ms_per_step": round(oel / k * 1e3, 4),
-                             "phases_ms": {kk: round(v, 4) for kk, v in octx.phase_times().items()},
-                             "equals_headline": keys(ores) == keys(res[:k]),
-                             "parity_vs_reference": (m.compress(G, ores[0]).hex() == want[0]) if want else None}
+            others[ometh[:4] + "_sync"] = leg(n * k / oel, oel / k * 1e3,
+                                             ((m.compress(G, ores[0]).hex() == want[0]) if want else True)
+                                             and keys(ores) == keys(res[:k]))
             octx.close()
 
     if world == 1 and not args.no_compare and not args.no_shards and G == 1 and args.log_n == 20 and batched:
         others.update(shard_legs(m, mdist, torch, dev, local, sp, host, K, W, n * K / elapsed))
     if world == 1 and not args.no_compare and not args.no_configs and G == 1 and args.log_n == 20:
-        others.update(config_legs(m, torch, dev, local, sp, pts, host, K, W))
+        others.update(config_legs(m, torch, dev, local, sp, pts, host, K, W, probe))
     # configs[3]: G1 n = 2^21 sharded over the ranks (RCCL path) or over the
     # shards of one process (--multi-context), against the golden 2^21 result
     if G == 1 and not args.no_compare and world > 1 and (1 << 21) % world == 0:
@@ -403,11 +423,10 @@ def main():
         h = ctx.params["h"]
         madds = n * h                                 # one table point per (i, j) digit
         alg_bytes = n * h * AFFINE_BYTES * G              # h affine gathers per pair (1184 B/pair incl. scalar)
-        workload = (f"G{G} MSM n=2^{args.log_n} per GPU, CHES nh+q/5 (q=2^{ctx.params['q_exp']}, h={h}, "
-                    f"|B|={ctx.params['b_size']}), table T=m*q^j*P_i resident in HBM, K distinct scalar sets "
-                    f"H2D from pinned host memory inside the timed region")
-        cfg_extra = {"method": "ches_q_over_5", "beta": beta,
-                     "config_file": f"ches_config_files/config_file_n_exp_{cfg_n}{'_beta' if beta else ''}.h",
+        workload = (f"G{G} MSM n=2^{args.log_n} per GPU, CHES nh+q/5, table in HBM, K distinct scalar sets H2D "
+                    f"from pinned host memory in the timed region")
+        cfg_extra = {"method": "ches_q_over_5",
+                     "config_file": f"config_file_n_exp_{cfg_n}{'_beta' if beta else ''}.h",
                      "q_exp": ctx.params["q_exp"], "h": h,
                      "bucket_set": ctx.params["b_size"], "buckets_incl_top_digit_copies": ctx.bucket_count()}
     elif args.method == "bgmw":
@@ -433,14 +452,34 @@ def main():
                 traffic = tj.get("accumulate_bytes_per_launch")
         except Exception:
             traffic = None
-    fpm_per_madd = FPMUL_PER_MADD if G == 1 else 28   # Fp2: 8M + 2S = 8*3 + 2*2 Fp-mul
-    fpmul_rate = madds * fpm_per_madd / acc_s
     mads, mads_src = isa_mads_per_madd(G)
+    acc_alone = phases.get("accumulate") and phases["accumulate"] / 1e3
+    # VALU roofline, priced against ceilings measured in THIS run on this device
+    # (msm_valu_probe, csrc/probe.hip): the register-resident G1 madd loop (the
+    # accumulation's body without its row loads) and the chip's v_mad_u64_u32
+    # rate.  G2 has no madd probe: its valu fraction is the mad fraction.
+    pk = probe or {"mad": MAD_RATE, "madd": MADD_RATE_R02, "fpmul": FPMUL_PEAK}
+    mad_frac = round(madds * mads / acc_s / pk["mad"], 4) if mads else None
+    mad_frac_alone = round(madds * mads / acc_alone / pk["mad"], 4) if mads and acc_alone else None
+    valu = {"valu_bound": "valu-int (v_mad_u64_u32 issue)",
+            "valu_unit": "G madd/s" if G == 1 else "T mad/s",
+            "valu_achieved": round(madds / acc_s / 1e9, 3) if G == 1 else round(madds * mads / acc_s / 1e12, 3),
+            "valu_peak": round(pk["madd"] / 1e9, 3) if G == 1 else round(pk["mad"] / 1e12, 3),
+            "valu_frac": round(madds / acc_s / pk["madd"], 4) if G == 1 else mad_frac,
+            "valu_frac_alone": (round(madds / acc_alone / pk["madd"], 4) if acc_alone else None) if G == 1
+            else mad_frac_alone,
+            "mad_frac": mad_frac, "mad_frac_alone": mad_frac_alone, "mads_per_madd": mads,
+            "mad_peak_T": round(pk["mad"] / 1e12, 3), "fpmul_peak_G": round(pk["fpmul"] / 1e9, 2),
+            "peak_basis": "this run (msm_valu_probe)" if probe else "round-2 constants (probe unavailable)"}
 
     parity = golden_ok if golden_ok is not None else cross
     if batch_eq_sync is False:
         parity = False
     line = {
+        "legs": dict(legs, **others),
+        "legs_key": "M = M pairs/s, ms = ms per MSM, ok = bit-exact vs the reference; DESIGN.md sec.13",
+        "phases_ms": [round(v, 4) for v in phases.values()],
+        "parity_detail": {"set0_golden": golden_ok, "batch_eq_sync": batch_eq_sync, "pip_cross_ranks": cross},
         "metric": METRIC if G == 1 else METRIC_G2,
         "value": round(value, 1),
         "unit": "pairs/s",
@@ -458,39 +497,13 @@ def main():
                         "parallelism": (f"one n=2^{args.log_n + world.bit_length() - 1} MSM: points sharded x{world}, "
                                         f"RCCL all_gather of {144 * G}-B partials" if world > 1 else "1 GPU")},
                        **cfg_extra),
-        "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved_gbs / HBM_PEAK_GBS, 5), "traffic": traffic,
-                     "kernel": "k_accumulate (bucket accumulation)", "kernel_ms": round(acc_s * 1e3, 4),
-                     "kernel_ms_basis": "HIP events around each accumulation of the timed batch, on its stream",
-                     "algorithmic_bytes_per_launch": alg_bytes,
-                     "note": "integer-VALU bound (v_mad_u64_u32 issue), see valu_roofline"},
-        "valu_roofline": {"bound": "valu-int", "achieved": round(fpmul_rate / 1e9, 2),
-                          "peak": round(FPMUL_PEAK / 1e9, 2), "unit": "G Fp-mul/s",
-                          "frac": round(fpmul_rate / FPMUL_PEAK, 4),
-                          "work": f"{madds} xyzz madds x {fpm_per_madd} Fp-mul",
-                          "peak_basis": "measured register-resident Fp-mul kernel (profiles/r02_fp_rate.txt)",
-                          "frac_alone": (round(madds * fpm_per_madd / (phases["accumulate"] / 1e3) / FPMUL_PEAK, 4)
-                                         if phases.get("accumulate") else None),
-                          "alone_basis": "the same kernel in one synchronous MSM (phases_ms.accumulate): no front or "
-                                         "reduction of a neighbouring MSM shares its SIMDs",
-                          # hardware-anchored: v_mad_u64_u32 issued per launch vs the measured chip mad rate
-                          "mad_frac": round(madds * mads / acc_s / MAD_RATE, 4) if mads else None,
-                          "mad_frac_alone": (round(madds * mads / (phases["accumulate"] / 1e3) / MAD_RATE, 4)
-                                             if mads and phases.get("accumulate") else None),
-                          "mads_per_madd": mads, "mad_rate_peak": MAD_RATE,
-                          "mad_basis": (f"{madds} madds x {mads} v_mad_u64_u32 (6 mul + 2 sqr + 1 two-product sum"
-                                        f"{'' if G == 1 else ' of Fp2 on a lane pair, both lanes'}, "
-                                        f"gfx950 ISA counts {mads_src}) / kernel time / {MAD_RATE / 1e12:.2f} T "
-                                        f"mad/s (profiles/r02_instr_rate.txt)")},
-        "phases_ms": {k: round(v, 4) for k, v in phases.items()},
-        "phases_note": "one synchronous MSM (profiled) after the timed region" if batched else "last timed step",
-        "pipelined_batch": batched,
-        "setup_batch": bool(batched and args.setup_batch),
-        "parity_vs_reference": parity,
-        "parity_detail": {"set0_vs_golden": golden_ok, "batch_equals_sync_all_sets": batch_eq_sync,
-                          "pippenger_cross_check_all_ranks": cross},
-        "methods": dict(legs, **others),
+        "roofline": dict({"bound": "hbm", "achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": round(achieved_gbs / HBM_PEAK_GBS, 5), "traffic": traffic,
+                          "kernel": "k_accumulate", "kernel_ms": round(acc_s * 1e3, 4),
+                          "kernel_ms_alone": round(acc_alone * 1e3, 4) if acc_alone else None,
+                          "algorithmic_bytes_per_launch": alg_bytes}, **valu),
         "cpu_baseline": cpu,
+        "parity_vs_reference": parity,
     }
     print(json.dumps(line), flush=True)
     if world > 1:
@@ -504,7 +517,7 @@ def _golden(m, G, n):
     return want[0] if want else None
 
 
-def config_legs(m, torch, dev, local, sp, pts, host, K, W):
+def config_legs(m, torch, dev, local, sp, pts, host, K, W, probe):
     """The other single-GPU BASELINE configs and the blst drop-in boundary, each
     timed and parity-checked against the reference's golden (set 0 = the seed-1
     stream, whose first 2^k scalars are the seed-1 set of 2^k points):
@@ -552,12 +565,8 @@ def config_legs(m, torch, dev, local, sp, pts, host, K, W):
         r, el = timed(lambda k: pc.mult(d16.data_ptr() + k * 32 * n16, 255, stride=32, on_device=True, stream=sp), K)
         pc.set_profiling(True)
         pc.mult(d16.data_ptr(), 255, stride=32, on_device=True, stream=sp)
-        legs[f"cfg1_pippenger_2^16_ctx_c{c}"] = {
-            "value": round(n16 * K / el, 1), "unit": "pairs/s", "ms_per_step": round(el / K * 1e3, 4),
-            "phases_ms": {kk: round(v, 4) for kk, v in pc.phase_times().items()},
-            "parity_vs_reference": m.compress(1, r[0]).hex() == want16,
-            "note": f"configs[1]: K synchronous msm_ctx_mult calls (per-MSM latency), window c={c}, points and "
-                    f"{K} scalar sets resident in HBM"}
+        legs[f"cfg1_ctx_c{c}"] = leg(n16 * K / el, el / K * 1e3, m.compress(1, r[0]).hex() == want16,
+                                     phases=[round(v, 4) for v in pc.phase_times().values()])
         # the same K sets through the pipelined batch (msm_ctx_mult_batch): throughput
         pc.mult_batch(d16.data_ptr(), K, 255, on_device=True, stream=sp)  # untimed: sizes the batch buffers
         torch.cuda.synchronize(dev)
@@ -565,23 +574,13 @@ def config_legs(m, torch, dev, local, sp, pts, host, K, W):
         rb = pc.mult_batch(d16.data_ptr(), K, 255, on_device=True, stream=sp)
         torch.cuda.synchronize(dev)
         elb = time.perf_counter() - t
-        legs[f"cfg1_pippenger_2^16_batch_c{c}"] = {
-            "value": round(n16 * K / elb, 1), "unit": "pairs/s", "ms_per_step": round(elb / K * 1e3, 4),
-            "parity_vs_reference": m.compress(1, rb[0]).hex() == want16,
-            "batch_equals_sync": [m.compress(1, x) for x in rb] == [m.compress(1, x) for x in r],
-            "note": f"configs[1]: one msm_ctx_mult_batch call over the same {K} resident sets, window c={c}, after "
-                    f"one untimed batch of {K}: fronts in groups of up to 4 sets, one accumulation launch per "
-                    f"group on two lanes, grouped reduction tails, host Horner of group q beside the GPU work "
-                    f"of later groups"}
+        legs[f"cfg1_batch_c{c}"] = leg(n16 * K / elb, elb / K * 1e3, m.compress(1, rb[0]).hex() == want16
+                                       and [m.compress(1, x) for x in rb] == [m.compress(1, x) for x in r])
         pc.close()
     for _ in range(max(W, 1)):
         dropin(1, P16, sets16[0], n16)
     r, el = timed(lambda k: dropin(1, P16, sets16[k], n16), K)
-    legs["cfg1_pippenger_2^16_blst_dropin"] = {
-        "value": round(n16 * K / el, 1), "unit": "pairs/s", "ms_per_step": round(el / K * 1e3, 4),
-        "parity_vs_reference": m.compress(1, r[0]).hex() == want16,
-        "note": "configs[1] through blst_p1s_mult_pippenger: {ptr, NULL} arrays in pageable host memory, points and "
-                "scalars uploaded by every call"}
+    legs["cfg1_dropin"] = leg(n16 * K / el, el / K * 1e3, m.compress(1, r[0]).hex() == want16)
     del d16
 
     # ---- the blst drop-in at 2^20 ----
@@ -592,11 +591,7 @@ def config_legs(m, torch, dev, local, sp, pts, host, K, W):
     for _ in range(max(W, 1)):
         dropin(1, P20, sets20[0], n20)
     r, el = timed(lambda k: dropin(1, P20, sets20[k], n20), k20)
-    legs["blst_p1s_mult_pippenger_2^20"] = {
-        "value": round(n20 * k20 / el, 1), "unit": "pairs/s", "ms_per_step": round(el / k20 * 1e3, 4),
-        "parity_vs_reference": m.compress(1, r[0]).hex() == _golden(m, 1, n20),
-        "note": "the drop-in boundary (pippenger_blst_built_in, main_p1.cpp:400-436): per call 96 MiB of points + "
-                "32 MiB of scalars from pageable host memory, digits/sort overlapping the point upload"}
+    legs["dropin20"] = leg(n20 * k20 / el, el / k20 * 1e3, m.compress(1, r[0]).hex() == _golden(m, 1, n20))
     # the same calls with the point array registered once (msm_register_host_table): no point upload
     L = m.lib()
     if L.msm_register_host_table(1, P20, n20) == 0:
@@ -604,11 +599,7 @@ def config_legs(m, torch, dev, local, sp, pts, host, K, W):
             dropin(1, P20, sets20[0], n20)
         r, el = timed(lambda k: dropin(1, P20, sets20[k], n20), k20)
         L.msm_unregister_host_table(P20)
-        legs["blst_p1s_mult_pippenger_2^20_registered"] = {
-            "value": round(n20 * k20 / el, 1), "unit": "pairs/s", "ms_per_step": round(el / k20 * 1e3, 4),
-            "parity_vs_reference": m.compress(1, r[0]).hex() == _golden(m, 1, n20),
-            "note": "the same drop-in calls after msm_register_host_table(P, n) once: the points are read from "
-                    "their device copy, only the 32 MiB of scalars cross PCIe per call"}
+        legs["dropin20_reg"] = leg(n20 * k20 / el, el / k20 * 1e3, m.compress(1, r[0]).hex() == _golden(m, 1, n20))
     del sets20, P20
 
     # ---- configs[0]: CPU reference at 2^10, and the drop-in at the same size ----
@@ -631,18 +622,11 @@ def config_legs(m, torch, dev, local, sp, pts, host, K, W):
             mult(rr, pp, n10, spp, 255, scratch)
             reps += 1
         el = time.perf_counter() - t
-        legs["cfg0_cpu_reference_2^10"] = {
-            "value": round(n10 * reps / el, 1), "unit": "pairs/s", "ms_per_step": round(el / reps * 1e3, 4),
-            "cores": 1, "parity_vs_reference": m.compress(1, bytes(rr)).hex() == want10,
-            "note": "configs[0]: the reference's own blst_p1s_mult_pippenger (libblst from /root/reference, "
-                    "oracle/_ref), 1 thread, the pippenger_blst_built_in call of ./run.sh config=10"}
+        legs["cfg0_cpu_ref"] = leg(n10 * reps / el, el / reps * 1e3, m.compress(1, bytes(rr)).hex() == want10)
     for _ in range(3):
         dropin(1, P10, S10, n10)
     r, el = timed(lambda k: dropin(1, P10, S10, n10), 20)
-    legs["cfg0_gpu_blst_dropin_2^10"] = {
-        "value": round(n10 * 20 / el, 1), "unit": "pairs/s", "ms_per_step": round(el / 20 * 1e3, 4),
-        "parity_vs_reference": m.compress(1, r[0]).hex() == want10,
-        "note": "the same 2^10 call through the GPU drop-in (launch/latency-bound at this size)"}
+    legs["cfg0_gpu_dropin"] = leg(n10 * 20 / el, el / 20 * 1e3, m.compress(1, r[0]).hex() == want10)
 
     # ---- the blst-level CHES tile (main_p1.cpp:249-291 call sequence) at 2^16 and 2^20 ----
     legs.update(tile_d_ches_legs(m, pts, host))
@@ -676,30 +660,20 @@ def config_legs(m, torch, dev, local, sp, pts, host, K, W):
     eq = [m.compress(2, x) for x in bh[:2]] == [m.compress(2, x) for x in sync] and \
         [m.compress(2, x) for x in br] == [m.compress(2, x) for x in bh]
     par = c2.params
-    legs["cfg4_g2_ches_batch_h2d"] = {
-        "value": round(n20 * k2 / elh, 1), "unit": "pairs/s", "ms_per_step": round(elh / k2 * 1e3, 4),
-        "kernel_ms": round(acc_h, 4),
-        "valu_frac_alone": round(n20 * par["h"] * 28 / (ph["accumulate"] / 1e3) / FPMUL_PEAK, 4),
-        "phases_ms_sync": {kk: round(v, 4) for kk, v in ph.items()},
-        "parity_vs_reference": m.compress(2, bh[0]).hex() == _golden(m, 2, n20), "batch_equals_sync": eq,
-        "setup_s": round(setup, 2),
-        "note": f"configs[4]: G2 n=2^20 CHES (q=2^{par['q_exp']}, h={par['h']}, |B|={par['b_size']}), table in HBM, "
-                f"{k2} distinct scalar sets in pinned host memory, H2D in the timed region"}
+    mads2, _ = isa_mads_per_madd(2)
+    legs["cfg4_g2_h2d"] = leg(n20 * k2 / elh, elh / k2 * 1e3, m.compress(2, bh[0]).hex() == _golden(m, 2, n20) and eq,
+                              kernel_ms=round(acc_h, 4), cfg=f"q{par['q_exp']}h{par['h']}",
+                              mad_frac_alone=(round(n20 * par["h"] * mads2 / (ph["accumulate"] / 1e3) / probe["mad"], 4)
+                                              if probe and mads2 else None),
+                              phases=[round(v, 4) for v in ph.values()])
     # the G2 blst drop-in at 2^20 (main_p2.cpp:424 pippenger_blst_built_in): points + scalars per call
     P2 = (ctypes.c_uint8 * (192 * n20)).from_buffer_copy(bytes(pts2_host))
     S2 = set_bytes(0, n20)
     dropin(2, P2, S2, n20)
     r2, el2 = timed(lambda k: dropin(2, P2, S2, n20), 3)
-    legs["blst_p2s_mult_pippenger_2^20"] = {
-        "value": round(n20 * 3 / el2, 1), "unit": "pairs/s", "ms_per_step": round(el2 / 3 * 1e3, 4),
-        "parity_vs_reference": m.compress(2, r2[0]).hex() == _golden(m, 2, n20),
-        "note": "the G2 drop-in boundary (pippenger_blst_built_in of main_p2.cpp:400-436): per call 192 MiB of "
-                "points + 32 MiB of scalars from pageable host memory"}
+    legs["g2_dropin20"] = leg(n20 * 3 / el2, el2 / 3 * 1e3, m.compress(2, r2[0]).hex() == _golden(m, 2, n20))
     del P2, pts2_host
-    legs["cfg4_g2_ches_batch_resident"] = {
-        "value": round(n20 * k2 / elr, 1), "unit": "pairs/s", "ms_per_step": round(elr / k2 * 1e3, 4),
-        "parity_vs_reference": m.compress(2, br[0]).hex() == _golden(m, 2, n20),
-        "note": "configs[4], the same sets resident in HBM"}
+    legs["cfg4_g2_res"] = leg(n20 * k2 / elr, elr / k2 * 1e3, m.compress(2, br[0]).hex() == _golden(m, 2, n20))
     c2.close()
     del d2
     return legs
@@ -776,14 +750,8 @@ def tile_d_ches_legs(m, pts, host):
         for _ in range(reps):
             L.blst_p1_tile_pippenger_d_CHES(ret, ptrs, ne, nh, signs, buckets, B, v2i, len(B), p["d_max"])
         el = (time.perf_counter() - t) / reps
-        legs[f"blst_p1_tile_pippenger_d_CHES_2^{lg}"] = {
-            "value": round(n / el, 1), "unit": "pairs/s", "ms_per_step": round(el * 1e3, 4),
-            "ctx_sync_ms": round(sync_ms, 4), "ratio_vs_ctx_sync": round(el * 1e3 / sync_ms, 2),
-            "host_prep_ms": round(prep * 1e3, 1), "entries": ne, "gathered_bytes": ne * 96,
-            "parity_vs_reference": m.compress(1, bytes(ret)).hex() == _golden(m, 1, n),
-            "note": f"main_p1.cpp:249-291 sequence (q=2^{p['q_exp']}, h={h}): digits + construct_nh (host, not timed), "
-                    f"then the timed blst_p1_tile_pippenger_d_CHES over {ne} row pointers into the host table; the "
-                    f"context's synchronous MSM on the same set for comparison (ctx_sync_ms, scalars H2D)"}
+        legs[f"tile{lg}"] = leg(n / el, el * 1e3, m.compress(1, bytes(ret)).hex() == _golden(m, 1, n),
+                                ratio=round(el * 1e3 / sync_ms, 2))
         # the same calls after registering the host table once (msm_register_host_table): row indices
         # instead of gathered rows
         t = time.perf_counter()
@@ -796,14 +764,8 @@ def tile_d_ches_legs(m, pts, host):
                 L.blst_p1_tile_pippenger_d_CHES(ret, ptrs, ne, nh, signs, buckets, B, v2i, len(B), p["d_max"])
             el = (time.perf_counter() - t) / reps
             L.msm_unregister_host_table(T)
-            legs[f"blst_p1_tile_pippenger_d_CHES_2^{lg}_registered"] = {
-                "value": round(n / el, 1), "unit": "pairs/s", "ms_per_step": round(el * 1e3, 4),
-                "ctx_sync_ms": round(sync_ms, 4), "ratio_vs_ctx_sync": round(el * 1e3 / sync_ms, 2),
-                "register_s": round(reg_s, 3),
-                "parity_vs_reference": m.compress(1, bytes(ret)).hex() == _golden(m, 1, n),
-                "note": f"the same tile calls after msm_register_host_table(1, T, {3 * n * h}) once (not timed): "
-                        f"the {ne} pointers travel as 4-B row indices into the device copy of T, no row gather; "
-                        f"the buckets are still exported into the caller's array as the reference leaves them"}
+            legs[f"tile{lg}_reg"] = leg(n / el, el * 1e3, m.compress(1, bytes(ret)).hex() == _golden(m, 1, n),
+                                        ratio=round(el * 1e3 / sync_ms, 2))
         del T, ptrs, nh, signs, buckets
     return legs
 
@@ -853,17 +815,9 @@ def shard_legs(m, mdist, torch, dev, local, sp, host, K, W, headline_value):
         worst = max(times)
         proj = n20 * K / worst
         folded = mdist.fold(parts0, add)
-        out[f"shards_2^20_over_{N}_one_gpu"] = {
-            "value": None, "projected_value": round(proj, 1), "unit": "pairs/s",
-            "per_shard_ms": round(worst / K * 1e3, 4), "shard_ms_all": [round(x / K * 1e3, 4) for x in times],
-            "efficiency": round(proj / (N * headline_value), 4),
-            "parity_vs_reference": m.compress(1, folded).hex() == want if want else None,
-            "batch_equals_sync_all_shards": all(eqs), "points_per_shard": n, "lanes": lanes,
-            "config": f"config_file_n_exp_{n_exp}{'_beta' if cbeta else ''}.h: q=2^{params['q_exp']}, h={params['h']}, "
-                      f"|B|={params['b_size']}", "setup_s": round(setup, 2),
-            "note": f"ONE-GPU PROJECTION, not a scaling number: the {N} shards of `bench.py --gpus {N}` run one after "
-                    f"another on device 0, each its own {K}-set H2D batch; projected_value = 2^20 x {K} / slowest "
-                    f"shard's batch time; efficiency = projected_value / ({N} x headline)"}
+        out[f"shard{N}"] = leg(proj, worst / K * 1e3, (m.compress(1, folded).hex() == want if want else None)
+                               and all(eqs), eff=round(proj / (N * headline_value), 4),
+                               cfg=f"q{params['q_exp']}h{params['h']}")
     return out
 
 
@@ -905,12 +859,8 @@ def weak_leg(m, mdist, torch, dev, local, sp, world, rank, K, W, xdev, add):
     want = _golden(m, 1, n * world)
     ok = all_true(m.compress(1, res[0]).hex() == want, world, xdev) if want else None
     ctx.close()
-    return {"ches_weak_2^20_per_rank": {
-        "value": round(n * world * K / b.elapsed, 1), "unit": "pairs/s", "ms_per_step": round(b.elapsed / K * 1e3, 4),
-        "n_total": n * world, "parity_vs_reference": ok, "batch_equals_sync_set0_all_ranks": eq,
-        "setup_s": round(setup, 2), "scaling": "weak",
-        "note": f"weak scaling: {world} ranks x 2^20 points (config_file_n_exp_20.h per rank), {K} distinct scalar "
-                f"sets H2D from pinned memory, one all_gather of the batch's partials"}}
+    return {"weak_2p20_per_rank": leg(n * world * K / b.elapsed, b.elapsed / K * 1e3, (ok is not False) and eq,
+                                      golden=ok is not None, setup_s=round(setup, 2))}
 
 
 def cfg3_ranks(m, mdist, torch, dev, local, sp, world, rank, K, W, xdev, add):
@@ -935,11 +885,7 @@ def cfg3_ranks(m, mdist, torch, dev, local, sp, world, rank, K, W, xdev, add):
     want = _golden(m, 1, N)
     ok = all_true(m.compress(1, res[0]).hex() == want, world, xdev)
     ctx.close()
-    return {"cfg3_2^21_ranks": {
-        "value": round(N * K / b.elapsed, 1), "unit": "pairs/s", "ms_per_step": round(b.elapsed / K * 1e3, 4),
-        "parity_vs_reference": ok, "setup_s": round(setup, 2), "points_per_rank": n,
-        "note": f"configs[3]: G1 n=2^21 over {world} ranks ({n} points each, config_file_n_exp_{n_exp}.h), "
-                f"{K} distinct scalar sets H2D from pinned memory, one all_gather of the batch's partials"}}
+    return {"cfg3_ranks": leg(N * K / b.elapsed, b.elapsed / K * 1e3, ok, setup_s=round(setup, 2))}
 
 
 def cfg3_multi_context(m, torch, D, one_device, K, W):
@@ -967,14 +913,8 @@ def cfg3_multi_context(m, torch, D, one_device, K, W):
     want = _golden(m, 1, N)
     eq = [m.compress(1, x) for x in sres] == [m.compress(1, x) for x in res[:len(sres)]]
     ctx.close()
-    return {"cfg3_2^21_multi_context": {
-        "value": round(N * K / el, 1), "unit": "pairs/s", "ms_per_step": round(el / K * 1e3, 4),
-        "sync_ms_per_msm": round(sel * 1e3, 4), "parity_vs_reference": m.compress(1, res[0]).hex() == want,
-        "batch_equals_sync": eq, "setup_s": round(setup, 2), "devices": devs,
-        "shards_merged": bool(one_device and D > 1 and os.environ.get("MSM_MULTI_MERGE", "1") != "0"),
-        "note": f"configs[3] in ONE process: {D} shards of {n} points (config_file_n_exp_{n_exp}.h) on devices "
-                f"{sorted(set(devs))}, msm_ches_ctx_create_multi, {K} distinct sets from pinned host memory; "
-                "shards sharing a device run as one engine over their joint range (csrc/multi.hpp)"}}
+    return {"cfg3_multi_ctx": leg(N * K / el, el / K * 1e3, m.compress(1, res[0]).hex() == want and eq,
+                                  sync_ms=round(sel * 1e3, 4), devices=len(set(devs)))}
 
 
 def _ref_lib(name):
@@ -1038,7 +978,10 @@ def cpu_baseline(m, pts, host, n, K, gpu_res, G, log_n):
         out = {"value": one["value"], "unit": "pairs/s", "cores": 1, "kind": kind,
                "sample": f"reference libblst blst_p{G}s_mult_pippenger (oracle/_ref), 1 thread, "
                          f"first 2^{log_n} points, scalar sets 0-{one['sets'] - 1}, {dt1:.1f}s",
-               "matches_gpu": one["matches_gpu"], "all_cores": multi}
+               "matches_gpu": one["matches_gpu"],
+               # the Go binding's tile grid (bindings/go/blst.go:2064-2197) on CPU_THREADS threads, last set
+               "all_cores_value": multi and multi["value"], "all_cores_cores": multi and multi["cores"],
+               "all_cores_matches_gpu": multi and multi["matches_gpu"]}
     else:
         sys.path.insert(0, os.path.join(REPO, "tests"))
         import oracle_ffi as of

@@ -192,6 +192,11 @@ int msm_set_abort_on_error(int on);
 /* nonzero if a blst-named call of this thread failed since the last query (clears it) */
 int msm_error_pending(void);
 int msm_device_count(void);
+/* The VALU ceilings of `device`, measured now by register-resident kernels
+ * (extension, no reference counterpart; bench.py prices its roofline with them
+ * in the same run): out = {v_mad_u64_u32 lane-ops/s, Fp-mul/s, G1 xyzz madd/s
+ * (the accumulation's loop body, rows in cache), device ms spent} */
+int msm_valu_probe(int device, double out[4]);
 /* Engines behind the blst-named entry points (no caller context: ref
  * multi_scalar.c:581-607) live in a process-wide pool per (device, kind,
  * window): a call leases one, a concurrent call creates another, and a returned
@@ -219,7 +224,10 @@ size_t msm_set_engine_cache_limit(size_t bytes);
  * uploading 96/192 B per point (ref multi_scalar.c:549-607; callers that
  * multiply one SRS many times).  The
  * caller must not modify or free the rows while they are registered (as with
- * hipHostRegister).  group 1 (G1, blst_p1_affine rows) or 2 (G2); registering
+ * hipHostRegister).  Guard: up to 1024 rows at even strides (first and last
+ * included) are sampled at registration; a call whose rows include a sample
+ * that no longer matches the host memory re-uploads the table first, so a
+ * reused or rewritten buffer is caught (an edit of one unsampled row is not).  group 1 (G1, blst_p1_affine rows) or 2 (G2); registering
  * an already registered base replaces it.  Returns MSM_OK or an error code. */
 int msm_register_host_table(int group, const void *rows_affine, size_t nrows);
 int msm_unregister_host_table(const void *rows_affine);
@@ -273,8 +281,9 @@ int msm_ches_ctx_create_params(msm_ches_ctx **ctx, int group, int device, const 
  * table rows and scalars must be in host memory when ndev > 1. */
 int msm_ches_ctx_create_multi(msm_ches_ctx **ctx, int group, const int *devices, int ndev, int n_exp, int beta);
 int msm_ches_ctx_shards(const msm_ches_ctx *ctx);
-/* 1 if this context's batches exchange their partials over RCCL (several
- * distinct devices, or MSM_MULTI_RCCL=1), 0 if each shard is read back */
+/* 1 if this context's batches exchange their partials over RCCL (opt-in:
+ * MSM_MULTI_RCCL=1 with shards on distinct devices; round 6 made it opt-in
+ * until a run on several devices has checked it), 0 if each shard is read back */
 int msm_ches_ctx_rccl_exchange(const msm_ches_ctx *ctx);
 /* base points P_i (blst affine) -> T built on the GPU */
 int msm_ches_ctx_build_table(msm_ches_ctx *ctx, const void *points_affine, size_t npoints, int on_device,

@@ -29,7 +29,7 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-
 # group in parallel (the G2 instantiations dominate the build time)
 SOURCES = [("engine.hip", 1), ("engine.hip", 2), ("ches.hip", 1), ("ches.hip", 2), ("bgmw.hip", 1), ("bgmw.hip", 2),
            ("compat.hip", 1), ("compat.hip", 2), ("wbits.hip", 1), ("wbits.hip", 2),
-           ("abi.cpp", None)]
+           ("probe.hip", None), ("abi.cpp", None)]
 
 
 def _deps():

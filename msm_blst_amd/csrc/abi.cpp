@@ -20,6 +20,7 @@
 #include "engine.hpp"
 #include "multi.hpp"
 #include "pool.hpp"
+#include "ptr_walk.hpp"
 #include "table_registry.hpp"
 
 using namespace msm;
@@ -73,43 +74,6 @@ std::unique_ptr<typename EnginePool<Pippenger<G>>::Lease> pippenger_engine(int w
                                                [&] { return std::make_unique<Pippenger<G>>(dev, window); });
 }
 
-// The n elements of `sz` bytes named by a blst pointer array, with the
-// reference's iteration rule (ref multi_scalar.c:390-416): the first pointer is
-// always taken; after it, a non-NULL entry names the next element and a NULL
-// entry means "the element right after the previous one" -- so {ptr, NULL} is
-// one flat array and a NULL after k explicit pointers continues contiguously.
-// Returns the elements as one contiguous host range: the caller's own memory
-// when they already are one (the flat case; no host copy at all), otherwise a
-// gather into `buf` that copies each run of adjacent elements with one memcpy.
-const uint8_t *contiguous(std::vector<uint8_t> &buf, const void *const *ptrs, size_t n, size_t sz) {
-  if (n == 0) return nullptr;
-  const uint8_t *base = (const uint8_t *)ptrs[0];
-  size_t i = 1;
-  const void *const *pp = ptrs + 1;
-  // walk the explicit pointers while they stay adjacent
-  while (i < n && *pp && (const uint8_t *)*pp == base + i * sz) ++i, ++pp;
-  if (i == n || !*pp) return base;  // all adjacent, or a NULL: the rest continues after the previous element
-  buf.resize(n * sz);
-  memcpy(buf.data(), base, i * sz);
-  const uint8_t *p = base + (i - 1) * sz;
-  while (i < n) {
-    if (!*pp) {  // the rest is contiguous after p
-      memcpy(buf.data() + i * sz, p + sz, (n - i) * sz);
-      break;
-    }
-    const uint8_t *run = (const uint8_t *)*pp++;
-    size_t k = 1;
-    while (i + k < n && *pp && (const uint8_t *)*pp == run + k * sz) ++k, ++pp;
-    if (i + k < n && !*pp) {  // a NULL right after the run extends it to the end
-      k = n - i;
-    }
-    memcpy(buf.data() + i * sz, run, k * sz);
-    p = run + (k - 1) * sz;
-    i += k;
-  }
-  return buf.data();
-}
-
 // The device rows of n points at `pts` when a registered host table holds all
 // of them (msm_register_host_table; table_registry.hpp), else nullptr.  `hold`
 // keeps the table alive for the call.
@@ -121,6 +85,8 @@ const void *registered_rows(const uint8_t *pts, size_t n, std::shared_ptr<HostTa
   if (!t) return nullptr;
   const size_t off = (size_t)(pts - t->base) / (96 * G);
   if (off + n > t->nrows) return nullptr;
+  t = fresh<G>(t, off, off + n - 1);  // rows edited since registration: re-uploaded
+  if (!t) return nullptr;
   hold = t;
   return t->rows.template as<uint8_t>() + off * t->row_bytes;
 }
@@ -701,6 +667,17 @@ int msm_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
   return n;
+}
+
+int msm_valu_probe(int device, double out[4]) {
+  if (!out) return fail(MSM_E_ARG, "null out");
+  if (msm_device_count() <= device || device < 0) return fail(MSM_E_NODEV, "no such HIP device");
+  try {
+    valu_probe(device, out);
+    return MSM_OK;
+  } catch (const std::exception &e) {
+    return fail(MSM_E_HIP, e.what());
+  }
 }
 
 int msm_ctx_create(msm_ctx **ctx, int group, int device, int window_bits) {

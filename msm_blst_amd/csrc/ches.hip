@@ -1211,18 +1211,21 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
   // to back beside the first five: 2^20 H2D 436.4 / 439.2 / 439.9 vs 432.4 /
   // 436.2 / 436.7 M pairs/s (L = 8 vs all at the start, tools/h2d_ab.py
   // medians, alternating on one box; profiles/r05_copy_pace_ab.txt).  The wait
-  // only ever targets work already enqueued (or an event of an earlier batch,
-  // which has completed), so it cannot deadlock; the host stays L MSMs ahead.
+  // targets MSM fgb[g] - L clamped to the last accumulation already enqueued in
+  // THIS batch (acc_enq; in the accumulation-group schedule front g is issued
+  // when only the groups up to g - nfr + 1 are enqueued), so it
+  // never waits on a stale or unrecorded event and cannot deadlock.
   static const size_t pace_env = [] {
     const char *e = getenv("MSM_COPY_PACE");
     return (size_t)(e ? std::max(0, std::min(32, atoi(e))) : 8);
   }();
   const size_t pace = scalars_on_host && !zero_copy && pace_env >= 3 ? pace_env : 0;
+  size_t acc_enq = 0;  // accumulations whose eva[] event is recorded in this batch
   auto front_group = [&](size_t g) {
     if (g >= nfg) return;
     const bool copied = scalars_on_host && !zero_copy;
     if (pace && g >= pace && g < nsg) {
-      MSM_HIP_CHECK(hipEventSynchronize(eva[fgb[g] - pace]));
+      if (acc_enq) MSM_HIP_CHECK(hipEventSynchronize(eva[std::min(fgb[g] - pace, acc_enq - 1)]));
       copy_group(g);
     }
     if (copied) MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, evc[g], 0));
@@ -1304,6 +1307,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
         prof_k.push_back(k0);
       }
       for (size_t k = k0; k < k1; ++k) MSM_HIP_CHECK(hipEventRecord(eva[k], L));
+      acc_enq = k1;
       for (size_t a = k0; a < k1;) {  // level 0, one launch per reduction group touched
         const size_t q = grp(a), b = std::min(k1, gfirst[q + 1]);
         if (q >= (size_t)nred) MSM_HIP_CHECK(hipStreamWaitEvent(L, evt[q - nred], 0));  // reducer set free again
@@ -1342,6 +1346,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
           prof_k.push_back(k);
         }
         MSM_HIP_CHECK(hipEventRecord(eva[k], L));
+        acc_enq = k + 1;
         red.launch_head_slot(L, buckets_[bset].p, gset, slot);
         MSM_HIP_CHECK(hipEventRecord(evh[k], L));
         if (gend(k)) {  // the group's level 0s are done on both lanes
@@ -1396,6 +1401,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
         prof_k.push_back(k);
       }
       MSM_HIP_CHECK(hipEventRecord(eva[k], s));
+      acc_enq = k + 1;
       if (k >= 1) {
         MSM_HIP_CHECK(hipEventRecord(evh[k - 1], s));
         l0_group_tail(k - 1);
@@ -1425,6 +1431,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
         prof_k.push_back(k);
       }
       MSM_HIP_CHECK(hipEventRecord(eva[k], s));
+      acc_enq = k + 1;
       MSM_HIP_CHECK(hipStreamWaitEvent(ts, eva[k], 0));
       red.launch_head_slot(ts, buckets_[bset].p, gset, slot);
       MSM_HIP_CHECK(hipEventRecord(evh[k], ts));

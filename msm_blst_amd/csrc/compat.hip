@@ -245,6 +245,7 @@ void entry_msm_ptrs(void *ret, const void *const *points, size_t ne, EntryFill f
   int dev = 0;
   MSM_HIP_CHECK(hipGetDevice(&dev));
   std::shared_ptr<HostTable> tab = TableRegistry::get().find(G, dev, points[0]);
+  if (tab) tab = fresh<G>(tab, 0, tab->nrows - 1);  // rows edited since registration: re-uploaded
   if (tab) {
     std::atomic<bool> outside{false};
     const uint8_t *base = tab->base;
@@ -353,6 +354,7 @@ void register_host_table(const void *rows, size_t nrows) {
   t->base = static_cast<const uint8_t *>(rows);
   t->nrows = nrows;
   t->row_bytes = sizeof(AffP<F>);
+  t->take_samples();  // before the upload: a concurrent edit then shows as stale next call
   t->rows.ensure(nrows * sizeof(AffP<F>));
   const size_t psz = 96 * G, chunk = std::min<size_t>(nrows, ((size_t)64 << 20) / psz);
   hipStream_t s;

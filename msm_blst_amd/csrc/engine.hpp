@@ -591,6 +591,9 @@ void entry_msm_ptrs(void *ret, const void *const *points, size_t ne, EntryFill f
 template <int G>
 void weighted_bucket_sum(void *ret_jac, const void *buckets_blst, size_t nb, const uint32_t *weights);
 
+// VALU ceilings of this device, measured now (probe.hip): {mad lane-ops/s,
+// Fp-mul/s, G1 madd/s, device ms spent}
+void valu_probe(int device, double out[4]);
 // device self-tests (engine.hip)
 template <int G>
 void test_field(int op, const uint64_t *a, const uint64_t *b, uint64_t *out, size_t n);

@@ -25,103 +25,9 @@
 #include <vector>
 
 #include "engine.hpp"
+#include "workers.hpp"  // WorkerPool
 
 namespace msm {
-
-// Process-wide pool of host worker threads (never destroyed: the workers park
-// on a condition variable for the life of the process).  parallel_for runs
-// f(0..n-1) on the workers and the calling thread and returns when all are
-// done; concurrent callers take turns.
-class WorkerPool {
- public:
-  static WorkerPool &get() {
-    static WorkerPool *p = new WorkerPool();
-    return *p;
-  }
-  size_t size() const { return th_.size() + 1; }
-
-  void parallel_for(size_t n, const std::function<void(size_t)> &f) {
-    if (n == 0) return;
-    if (n == 1 || th_.empty()) {
-      for (size_t i = 0; i < n; ++i) f(i);
-      return;
-    }
-    std::lock_guard<std::mutex> turn(call_mu_);
-    auto job = std::make_shared<Job>();
-    job->f = &f;
-    job->n = n;
-    job->remaining = n;
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      job_ = job;
-      ++gen_;
-    }
-    cv_.notify_all();
-    run(*job);
-    {
-      std::unique_lock<std::mutex> lk(job->mu);
-      job->done.wait(lk, [&] { return job->remaining == 0; });
-    }
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      job_.reset();
-    }
-    if (job->err) std::rethrow_exception(job->err);
-  }
-
- private:
-  struct Job {
-    const std::function<void(size_t)> *f = nullptr;
-    size_t n = 0;
-    std::atomic<size_t> next{0};
-    size_t remaining = 0;  // guarded by mu
-    std::exception_ptr err;
-    std::mutex mu;
-    std::condition_variable done;
-  };
-  std::mutex call_mu_, mu_;
-  std::condition_variable cv_;
-  std::shared_ptr<Job> job_;
-  uint64_t gen_ = 0;
-  std::vector<std::thread> th_;
-
-  WorkerPool() {
-    // the box's CPU share per GPU is 16 threads; host copies saturate at ~8
-    // (h2d_stage: 142 GB/s memcpy into pinned memory with 8 threads)
-    size_t want = 7;
-    if (const char *e = getenv("MSM_HOST_THREADS")) want = (size_t)std::max(1, atoi(e)) - 1;
-    const size_t hw = std::thread::hardware_concurrency();
-    if (hw) want = std::min(want, hw > 1 ? hw - 1 : 0);
-    for (size_t t = 0; t < want; ++t) th_.emplace_back([this] { loop(); });
-    for (auto &t : th_) t.detach();
-  }
-  static void run(Job &j) {
-    size_t i;
-    while ((i = j.next.fetch_add(1)) < j.n) {
-      try {
-        (*j.f)(i);
-      } catch (...) {
-        std::lock_guard<std::mutex> g(j.mu);
-        if (!j.err) j.err = std::current_exception();
-      }
-      std::lock_guard<std::mutex> g(j.mu);
-      if (--j.remaining == 0) j.done.notify_all();
-    }
-  }
-  void loop() {
-    uint64_t seen = 0;
-    for (;;) {
-      std::shared_ptr<Job> j;
-      {
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return gen_ != seen; });
-        seen = gen_;
-        j = job_;
-      }
-      if (j) run(*j);  // a stale job has next >= n: nothing to do
-    }
-  }
-};
 
 // memcpy of `bytes` split over the worker pool (1-MiB pieces or more)
 inline void parallel_memcpy(void *dst, const void *src, size_t bytes) {

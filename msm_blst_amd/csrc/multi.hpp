@@ -14,15 +14,16 @@
 // thread per shard per call was a visible fixed cost at 2^18 points per GPU,
 // where one MSM takes < 1 ms), and host scalars reach each device through the
 // shard's pinned ring (hoststage.hpp) instead of a pageable copy.
-// Batches on several DISTINCT devices exchange over RCCL (the north star's
-// "single RCCL reduce of the partial sums over xGMI"): every shard leaves its
+// Batches on several DISTINCT devices can exchange over RCCL (the north star's
+// "single RCCL reduce of the partial sums over xGMI"; opt-in since round 6,
+// MSM_MULTI_RCCL=1, until a run on several devices has checked it): every shard leaves its
 // per-MSM window sums (2 Jacobians, 288 B G1 / 576 B G2, per MSM) in a device
 // exchange buffer, ONE ncclGather collects all shards' buffers on the first
 // shard's device, one read-back, and the host combines and folds them exactly
 // (RCCL's reduction ops cannot add curve points, hence gather + fold).
-// MSM_MULTI_RCCL=0 reads every shard back separately instead (host fold of
-// the shards' own read-backs); =1 forces the RCCL exchange for any context of
-// distinct devices, including a single shard (how one GPU tests it).  Single
+// By default every shard is read back separately (host fold of the shards'
+// own read-backs); MSM_MULTI_RCCL=1 selects the RCCL exchange for any context
+// of distinct devices, including a single shard (how one GPU tests it).  Single
 // MSMs (run) keep the per-shard read-back: their latency path.  The reference
 // itself is single-device; its Go binding splits points x windows over threads
 // (bindings/go/blst.go:2064-2197), which would replicate points and tables on
@@ -52,6 +53,7 @@
 
 #include "engine.hpp"
 #include "hoststage.hpp"
+#include "workers.hpp"
 
 namespace msm {
 
@@ -67,16 +69,6 @@ class ChesMulti {
     DevBuf scal;               // host scalars of this shard, per call
     HostStager stage;          // pinned ring for those scalars
     hipStream_t stream = nullptr;  // the shard's own stream (shards may share a device)
-  };
-  // one persistent host thread per shard (several shards): each() hands every
-  // worker the same task and waits for all of them
-  struct Worker {
-    std::thread th;
-    std::mutex mu;
-    std::condition_variable cv;
-    std::function<void()> task;
-    bool has = false, quit = false, done = false;
-    std::exception_ptr err;
   };
 
   ChesMulti(const std::vector<int> &devices, const ChesParams &p) : p_(p), nlogical_(devices.size()) {
@@ -100,10 +92,8 @@ class ChesMulti {
           MSM_HIP_CHECK(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
         }
       }
-      if (groups.size() > 1) {
-        workers_ = std::vector<Worker>(groups.size());
-        for (Worker &w : workers_) w.th = std::thread([&w] { work(w); });
-      }
+      // one persistent host thread per shard (several shards; workers.hpp)
+      if (groups.size() > 1) team_ = std::make_unique<ThreadTeam>(groups.size());
     } catch (...) {
       release();  // the destructor does not run for a constructor that throws
       throw;
@@ -266,8 +256,7 @@ class ChesMulti {
     }
     n_ = n;
   }
-  std::vector<Worker> workers_;  // one per shard when there are several
-  std::mutex each_mu_;           // one each() at a time per context
+  std::unique_ptr<ThreadTeam> team_;  // one thread per shard when there are several (one run at a time)
   // RCCL exchange of batch partials (use_rccl): one communicator per shard
   // device (ncclCommInitAll, created at the first exchange), the shards' send
   // buffers and the gather buffer on shard 0's device
@@ -281,11 +270,14 @@ class ChesMulti {
       const char *e = getenv("MSM_MULTI_RCCL");
       return e ? atoi(e) : -1;
     }();
-    if (env == 0 || shards_.empty()) return false;
+    // opt-in (MSM_MULTI_RCCL=1): every run so far had one GPU, so the gather has
+    // only run on one-rank communicators; the per-shard read-back stays the
+    // default until a run on several devices has compared the two
+    if (env != 1 || shards_.empty()) return false;
     for (size_t a = 0; a < shards_.size(); ++a)  // distinct devices only (one rank per device)
       for (size_t b = a + 1; b < shards_.size(); ++b)
         if (shards_[a].device == shards_[b].device) return false;
-    return env == 1 || shards_.size() > 1;
+    return true;
   }
   static void nccl_check(ncclResult_t r, const char *what) {
     if (r != ncclSuccess) throw std::runtime_error(std::string("RCCL ") + what + ": " + ncclGetErrorString(r));
@@ -322,6 +314,9 @@ class ChesMulti {
       DeviceGuard dg(shards_[0].device);
       xrecv_.ensure(D * count * ob);
     }
+    // prior work on the caller's stream (which may write the scalar sets) is
+    // done before any shard reads them: the shards run on their own streams
+    MSM_HIP_CHECK(hipStreamSynchronize(s));
     each([&](Shard &sh) {
       const size_t g = &sh - shards_.data();
       DeviceGuard dg(sh.device);
@@ -351,7 +346,6 @@ class ChesMulti {
         MSM_HIP_CHECK(hipStreamSynchronize(shards_[g].stream));
       }
     }
-    (void)s;
     for (size_t k = 0; k < count; ++k) {
       std::vector<hfp::Jac<HF>> col(D);
       for (size_t g = 0; g < D; ++g) {
@@ -365,40 +359,8 @@ class ChesMulti {
     }
   }
 
-  static void work(Worker &w) {
-    for (;;) {
-      std::function<void()> t;
-      {
-        std::unique_lock<std::mutex> lk(w.mu);
-        w.cv.wait(lk, [&] { return w.has || w.quit; });
-        if (w.quit) return;
-        t = std::move(w.task);
-        w.has = false;
-      }
-      std::exception_ptr err;
-      try {
-        t();
-      } catch (...) {
-        err = std::current_exception();
-      }
-      {
-        std::lock_guard<std::mutex> g(w.mu);
-        w.err = err;
-        w.done = true;
-      }
-      w.cv.notify_all();
-    }
-  }
   void release() {
-    for (Worker &w : workers_) {
-      {
-        std::lock_guard<std::mutex> g(w.mu);
-        w.quit = true;
-      }
-      w.cv.notify_all();
-      if (w.th.joinable()) w.th.join();
-    }
-    workers_.clear();
+    team_.reset();  // joins the shard threads
     for (Shard &s : shards_)
       if (s.stream) {
         int prev = -1;
@@ -414,29 +376,11 @@ class ChesMulti {
   // exception is rethrown
   template <class Fn>
   void each(Fn f) {
-    if (workers_.empty()) {
+    if (!team_) {
       for (Shard &sh : shards_) f(sh);
       return;
     }
-    std::lock_guard<std::mutex> turn(each_mu_);
-    for (size_t g = 0; g < shards_.size(); ++g) {
-      Worker &w = workers_[g];
-      {
-        std::lock_guard<std::mutex> lk(w.mu);
-        w.task = [&f, this, g] { f(shards_[g]); };
-        w.has = true;
-        w.done = false;
-        w.err = nullptr;
-      }
-      w.cv.notify_all();
-    }
-    std::exception_ptr first;
-    for (Worker &w : workers_) {
-      std::unique_lock<std::mutex> lk(w.mu);
-      w.cv.wait(lk, [&] { return w.done; });
-      if (w.err && !first) first = w.err;
-    }
-    if (first) std::rethrow_exception(first);
+    team_->run([&](size_t g) { f(shards_[g]); });
   }
   // split a reference-layout row range over the owning shards:
   // f(shard, first row within the shard, rows, offset into the caller's range)

@@ -10,6 +10,12 @@
 // (compat.hip entry_msm_ptrs); a flat point array inside one feeds the plain
 // drop-in and its tiles without an upload (abi.cpp).  Process-wide, thread-safe; a call holds a
 // shared_ptr to the table it uses, so unregistering during a call is safe.
+//
+// Staleness guard (round 6, row_samples.hpp): every call through a table
+// compares the rows sampled at registration with the caller's memory and
+// re-uploads the table on a mismatch (fresh()).  Bulk rewrites and reused
+// buffers are caught; an edit of a single unsampled row is not -- the header's
+// contract (do not modify registered rows) still holds.
 #pragma once
 #include <stdint.h>
 
@@ -18,13 +24,12 @@
 #include <vector>
 
 #include "engine.hpp"
+#include "row_samples.hpp"
 
 namespace msm {
 
-struct HostTable {
-  int group = 1, device = 0;
-  const uint8_t *base = nullptr;  // caller's rows (blst affine, 96 G bytes each)
-  size_t nrows = 0;
+struct HostTable : RowSamples {  // group, base, nrows + the staleness samples (row_samples.hpp)
+  int device = 0;
   DevBuf rows;  // AffP<F> rows on `device`
   size_t row_bytes = 0;  // sizeof(AffP<F>)
 };
@@ -73,5 +78,15 @@ class TableRegistry {
 // upload + convert rows [rows, rows + nrows) to the current device (compat.hip)
 template <int G>
 void register_host_table(const void *rows, size_t nrows);
+
+// t, or -- when a sampled row in [lo, hi] no longer matches the host memory --
+// the table re-uploaded from the host rows (the registry entry is replaced)
+template <int G>
+std::shared_ptr<HostTable> fresh(std::shared_ptr<HostTable> t, size_t lo, size_t hi) {
+  if (!t || !t->changed(lo, hi)) return t;
+  DeviceGuard g(t->device);
+  register_host_table<G>(t->base, t->nrows);
+  return TableRegistry::get().find(G, t->device, t->base);
+}
 
 }  // namespace msm

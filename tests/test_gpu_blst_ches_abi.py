@@ -196,3 +196,48 @@ def test_registered_table_tiles(env):
     assert L.msm_unregister_host_table(T) != 0  # not registered any more
     env.fn("blst_p{g}_tile_pippenger_d_CHES")(ret, ptrs, n * h, nh, signs, ref_buckets, B, v2i, len(B), 6)
     assert m.compress(G, bytes(ret)).hex() == run["pippenger"]
+
+
+def test_registered_table_row_edited(env):
+    """The staleness guard of a registered table (row_samples.hpp): one row of
+    the registered host table edited between tile calls -- a row some entry
+    points at and that the guard samples (rows i (R - 1) / (k - 1), k = min(R,
+    1024)) -- must give what the gather path gives over the edited table (the
+    reference reads the host rows on every call, main_p1.cpp:279-282); the
+    restored row gives the golden again."""
+    m, G, g, T, B, H, v2i = env.m, env.G, env.g, env.T, env.B, env.H, env.v2i
+    L = m.lib()
+    n, h, qe = g["n"], g["h"], g["q_exp"]
+    run = _runs(g)[0]
+    nh = _std_digits(m.gen_scalars(n, run["seed"]), n, qe, h)
+    signs = (ctypes.c_ubyte * (n * h))()
+    ptrs = (ctypes.c_void_p * (n * h))()
+    env.fn("blst_p{g}_construct_nh_scalars_nh_points")(nh, signs, ptrs, n * h, T, H)
+    psz, R = 96 * G, 3 * n * h
+    k = min(R, 1024)
+    sampled = {i * (R - 1) // (k - 1) for i in range(k)}
+    base = ctypes.addressof(T)
+    row = next(r for r in ((p - base) // psz for p in ptrs) if r in sampled)
+    other = (row + 1) % R
+    saved = ctypes.string_at(base + row * psz, psz)
+
+    def tile():
+        bk = (ctypes.c_uint8 * (192 * G * len(B)))()
+        ret = (ctypes.c_uint8 * (144 * G))()
+        env.fn("blst_p{g}_tile_pippenger_d_CHES")(ret, ptrs, n * h, nh, signs, bk, B, v2i, len(B), 6)
+        return m.compress(G, bytes(ret)).hex()
+
+    assert L.msm_register_host_table(G, T, R) == 0, L.msm_last_error()
+    try:
+        assert tile() == run["pippenger"]
+        ctypes.memmove(base + row * psz, ctypes.string_at(base + other * psz, psz), psz)
+        edited = tile()
+        assert edited != run["pippenger"]
+        assert L.msm_unregister_host_table(T) == 0
+        assert tile() == edited  # the gather path over the edited host table
+        assert L.msm_register_host_table(G, T, R) == 0
+        ctypes.memmove(base + row * psz, saved, psz)
+        assert tile() == run["pippenger"]
+    finally:
+        ctypes.memmove(base + row * psz, saved, psz)
+        L.msm_unregister_host_table(T)

@@ -96,3 +96,45 @@ def test_c_abi_multi_device_rccl_gather(golden):
         assert rccl == 1, "the RCCL exchange was not selected"
         assert set0 == want[group]
         assert same
+
+
+CHILD_ORDER = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+import numpy as np, torch
+torch.cuda.init()
+import msm_blst_amd as m
+n, K = 1 << 16, 4
+ctx = m.CHESContext(1, n_exp=16, devices=[0])
+ctx.build_table(m.fixed_points(1, n), n)
+raw = b"".join(bytes(m.gen_scalars(n, 1 if k == 0 else 70 + k)) for k in range(K))
+host = torch.tensor(np.frombuffer(raw, dtype=np.uint8)).pin_memory()
+s = torch.cuda.Stream()
+with torch.cuda.stream(s):
+    d = torch.empty_like(host, device="cuda:0")
+    x = torch.randn(4096, 4096, device="cuda:0")
+    for _ in range(30):                   # keep the caller's stream busy ...
+        x = (x @ x).clamp_(-1, 1)
+    d.copy_(host, non_blocking=True)      # ... so the sets land late on it
+    got = [m.compress(1, r).hex() for r in ctx.mult_batch(d.data_ptr(), K, on_device=True, stream=s.cuda_stream)]
+torch.cuda.synchronize()
+want = [m.compress(1, ctx.mult(raw[32 * n * k:32 * n * (k + 1)])).hex() for k in range(K)]
+print("RESULT", [got[0], got == want, m.lib().msm_ches_ctx_rccl_exchange(ctx._ctx)])
+"""
+
+
+def test_rccl_batch_waits_for_the_callers_stream(golden):
+    """the RCCL exchange path (forced, one device) reads device
+    scalar sets that the caller's stream is still writing; it must order after
+    that stream (multi.hpp run_batch_rccl syncs it first).  The copy is queued
+    behind 30 GEMMs on the caller's stream; every result must equal the
+    synchronous MSM and set 0 the golden."""
+    want = [c["compressed"] for c in golden("msm_g1.json")["cases"]
+            if c["n"] == 1 << 16 and c["seed"] == 1 and c["case"] == "rand" and c["nbits"] == 255][0]
+    env = dict(os.environ, MSM_MULTI_RCCL="1")
+    r = subprocess.run([sys.executable, "-c", CHILD_ORDER, REPO], capture_output=True, text=True, env=env, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")]
+    assert line, r.stdout[-2000:] + r.stderr[-2000:]
+    set0, same, rccl = eval(line[0][7:])  # noqa: S307 -- our own child's repr of a list of str/bool/int
+    assert rccl == 1 and set0 == want and same

@@ -67,3 +67,49 @@ def test_registered_points_dropin(golden, points, group, n):
     finally:
         L.msm_unregister_host_table(P)
     assert _mult(m, group, base, n, sc) == want_full
+
+
+@pytest.mark.parametrize("group,n", [(1, 4096), (2, 1024)])
+def test_registered_rows_edited_between_calls(golden, points, group, n):
+    """The staleness guard (row_samples.hpp, ADVICE/VERDICT r05): the reference
+    reads the caller's points on every call (ref multi_scalar.c:549-607), so a
+    registered array whose rows change between calls must give the MSM of the
+    NEW rows.  Edits of a sampled row (the first and the last row are always
+    sampled) and a wholesale rewrite of the buffer (a reused allocation) are
+    each followed by a call that must equal the oracle's MSM of the edited
+    points; restoring the rows gives the golden again."""
+    import oracle_ffi as of
+
+    import msm_blst_amd as m
+    L = m.lib()
+    psz = 96 * group
+    orig = bytes(points(group, n + 1))
+    P = (ctypes.c_uint8 * (psz * n)).from_buffer_copy(orig[:psz * n])
+    base = ctypes.addressof(P)
+    sc = (ctypes.c_uint8 * (32 * n)).from_buffer_copy(m.gen_scalars(n, 1))
+    want = _golden(golden, group, n)
+
+    def oracle_of(buf):
+        return of.compress(group, of.msm(group, buf, sc, n))
+
+    assert L.msm_register_host_table(group, P, n) == 0, L.msm_last_error()
+    try:
+        assert _mult(m, group, base, n, sc) == want
+        for row in (0, n - 1):  # one row edited in place: the point of row (row + 1) % n
+            src = ((row + 1) % n) * psz
+            ctypes.memmove(base + row * psz, orig[src:src + psz], psz)
+            assert _mult(m, group, base, n, sc) == oracle_of(P)
+            ctypes.memmove(base + row * psz, orig[row * psz:(row + 1) * psz], psz)
+            assert _mult(m, group, base, n, sc) == want
+        # the whole buffer reused for another point set: P_1 .. P_n
+        ctypes.memmove(base, orig[psz:psz * (n + 1)], psz * n)
+        assert _mult(m, group, base, n, sc) == oracle_of(P)
+        assert _tile(m, group, base, n, sc, 16, 8) == _tile_unregistered(m, group, P, n, sc, 16, 8)
+    finally:
+        L.msm_unregister_host_table(P)
+
+
+def _tile_unregistered(m, group, P, n, sc, bit0, window):
+    """the same tile over a private copy of the rows (never registered)"""
+    Q = (ctypes.c_uint8 * len(P)).from_buffer_copy(bytes(P))
+    return _tile(m, group, ctypes.addressof(Q), n, sc, bit0, window)

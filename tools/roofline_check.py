@@ -32,7 +32,7 @@ out = {
     "bench_kernel_ms": line["roofline"]["kernel_ms"],
     "rocprof_vs_bench": round(avg / line["roofline"]["kernel_ms"], 4),
     "achieved_gbs_rocprof": round(alg / avg / 1e6, 2), "frac_rocprof": round(alg / avg / 1e6 / line["roofline"]["peak"], 5),
-    "valu_frac_rocprof": round(line["valu_roofline"]["frac"] * line["roofline"]["kernel_ms"] / avg, 4),
+    "valu_frac_rocprof": round(line["roofline"]["valu_frac"] * line["roofline"]["kernel_ms"] / avg, 4),
     "vgpr": timed[0]["VGPR_Count"], "scratch": timed[0]["Scratch_Size"],
 }
 js = json.dumps(out, indent=1)
