@@ -66,7 +66,9 @@ DEFAULT_BETA = {(2, 20): 1}
 # for any point count): the strong-scaling shards of `--gpus N` (2^20 / N points per rank) take the
 # configuration MEASURED fastest for that shard size on MI355X (tools/shard_study.py,
 # profiles/r05_shard_pip_study.txt), not necessarily the reference's config_file_n_exp_<log2 shard>.h
-SHARD_CONFIG = {}
+# round 6 (profiles/r06_tail_ab.txt, one box, two rounds): the 2^17 shard runs 0.410 ms per MSM with q = 2^19
+# (config_file_n_exp_17_beta.h: h = 14, |B| = 109 244) vs 0.425 with q = 2^20; 2^18 keeps q = 2^20 (0.668 vs 0.721)
+SHARD_CONFIG = {17: (17, 1)}
 
 
 def ches_config(log_n, beta=None, group=1):

@@ -150,11 +150,26 @@ static void launch_segsum_tail(hipStream_t s, const Xyzz<typename FieldOf<G>::F>
 }
 
 // -------------------------------------------------------------- scan reduce --
+// coop levels of the dense stage: only those with at most this many adds.  A
+// 4-wave add is the shortest latency for a narrow level, but its waves are 4x
+// the one-lane form's: a suffix step over a batch group's 20 x 2 x 1024 slots
+// ran 24 us per level coop (0.8 rounds of wave slots, 2.5 waves per SIMD
+// sharing issue) -- the batch's last, exposed tail (profiles/r06_small_trace.txt).
+// MSM_DENSE_COOP_MAX=<adds> overrides (0: every level one lane per add).
+static size_t dense_coop_max() {
+  static const size_t v = [] {
+    const char *e = getenv("MSM_DENSE_COOP_MAX");
+    return e ? (size_t)std::max(0, atoi(e)) : (size_t)16384;
+  }();
+  return v;
+}
+
 template <int G>
-void ScanReducer<G>::launch(hipStream_t s, const void *Abuf, int W, int S, bool coop) {
+void ScanReducer<G>::launch(hipStream_t s, const void *Abuf, int W, int S, bool coop_req) {
   typedef typename FieldOf<G>::F F;
   if (S < 1 || (S & (S - 1))) throw std::runtime_error("ScanReducer: S must be a power of two");
   const size_t NT = (size_t)W * S;
+  bool coop = coop_req && NT <= dense_coop_max();  // the suffix steps: NT adds each
   buf[0].ensure(NT * sizeof(Xyzz<F>));
   buf[1].ensure(NT * sizeof(Xyzz<F>));
   fin.ensure((size_t)W * 144 * G);
@@ -177,6 +192,7 @@ void ScanReducer<G>::launch(hipStream_t s, const void *Abuf, int W, int S, bool 
   }
   for (size_t len = NT; len > (size_t)W; len >>= 1) {  // sum_k T_k = sum_b b A_b
     Xyzz<F> *dst = buf[cur].as<Xyzz<F>>();
+    coop = coop_req && len / 2 <= dense_coop_max();  // this pair step: len / 2 adds
     if constexpr (G == 2) {
       if (coop)
         hipLaunchKernelGGL(k_pair_step_c2p, dim3(nblk(len / 2, 32)), dim3(256), 0, s, src, dst, len / 2);
@@ -353,6 +369,9 @@ void WeightedReducer<G>::plan(const std::vector<uint32_t> &w, const std::vector<
   for (size_t l = 0; l + 1 < bnout_.size(); ++l) maxp_ = std::max(maxp_, bnout_[l]);  // bit phase levels
   maxp1_ = 1;  // batch group tails: level l writes part_[l & 1]; the odd levels are at most half of level 0
   for (size_t l = 1; l + 1 < nout_.size(); l += 2) maxp1_ = std::max(maxp1_, nout_[l]);
+  // (the group bit tail, launch_tail_group_bits, alternates its levels over both
+  // part_ buffers: every bit level fits either)
+  for (size_t l = 0; l + 1 < bnout_.size(); ++l) maxp1_ = std::max(maxp1_, bnout_[l]);
   for (int st = 0; st < NSETS; ++st) {  // a new plan: sets are (re)sized on their next use
     part_[st][0].release();
     part_[st][1].release();
@@ -434,6 +453,7 @@ void WeightedReducer<G>::ensure_group(int set, int nmsm) {
   if (set < 0 || set >= NSETS || nmsm < 1) throw std::runtime_error("WeightedReducer: bad group");
   part_[set][0].ensure((size_t)nmsm * maxp_ * sizeof(Xyzz<F>));
   part_[set][1].ensure((size_t)nmsm * maxp1_ * sizeof(Xyzz<F>));
+  if (bits_) bgfin_[set].ensure((size_t)nmsm * bit_bytes());
   dense_buf_[set].ensure((size_t)nmsm * dense_slots() * sizeof(Xyzz<F>));
   const size_t NT = (size_t)nmsm * dense_slots();  // ScanReducer::launch's buffers for W = 2 nwin nmsm
   dense_[set].buf[0].ensure(NT * sizeof(Xyzz<F>));
@@ -489,6 +509,67 @@ void WeightedReducer<G>::launch_tail_group(hipStream_t s, int set, int nmsm, boo
     src = dst;
   }
   dense_[set].launch(s, dense_buf_[set].p, 2 * nwin_ * nmsm, 1 << sbits_, coop);
+}
+
+// The group tail ending in bit sums (one-window plans): the segment levels,
+// then per MSM the 2 s bit sums B_j (the bit phase of launch_tail, every level
+// one launch for the group), finalized to nmsm x 2 s Jacobians; the host
+// combines T = sum_j 2^j B_j (combine_bits).  ~10 levels instead of the 2 s of
+// the dense stage: for the batch's LAST group, whose tail runs after the last
+// accumulation with the chip otherwise idle (Ches::run_jobs).
+template <int G>
+void WeightedReducer<G>::launch_tail_group_bits(hipStream_t s, int set, int nmsm, bool coop) {
+  typedef typename FieldOf<G>::F F;
+  const size_t L = nout_.size(), LB = bnout_.size();
+  if (!has_bit_tail()) throw std::runtime_error("WeightedReducer: no bit tail in this plan");
+  const Xyzz<F> *src = part_[set][0].as<Xyzz<F>>();
+  size_t sstride = maxp_;
+  int cur = 0;
+  for (size_t l = 1; l + 1 < L; ++l) {  // segment levels 1 .. L-2 (L-1 is the dense scatter)
+    Xyzz<F> *dst = part_[set][l & 1].as<Xyzz<F>>();
+    const size_t dstride = (l & 1) ? maxp1_ : maxp_;
+    if (nout_[l]) launch_segsum_tail<G>(s, src, nullptr, starts_[l].as<uint32_t>(), dst, nout_[l], coop, nmsm, sstride,
+                                        dstride);
+    MSM_HIP_CHECK(hipGetLastError());
+    src = dst;
+    sstride = dstride;
+    cur = (int)(l & 1);
+  }
+  for (size_t l = 0; l < LB; ++l) {
+    const bool last = l + 1 == LB;
+    const int nb = cur ^ 1;
+    Xyzz<F> *dst = last ? dense_buf_[set].as<Xyzz<F>>() : part_[set][nb].as<Xyzz<F>>();
+    const size_t dstride = last ? bit_slots() : nb ? maxp1_ : maxp_;
+    const uint32_t *ix = l == 0 ? idx_.as<uint32_t>() + bidx_off_ : last ? idx_.as<uint32_t>() + bperm_off_ : nullptr;
+    if (bnout_[l])
+      launch_segsum_tail<G>(s, src, ix, bstarts_[l].as<uint32_t>(), dst, bnout_[l], coop, nmsm, sstride, dstride);
+    MSM_HIP_CHECK(hipGetLastError());
+    src = dst;
+    sstride = dstride;
+    cur = nb;
+  }
+  const int W = (int)((size_t)nmsm * bit_slots());
+  hipLaunchKernelGGL(k_finalize<G>, dim3(nblk((size_t)W, 64)), dim3(64), 0, s, src, bgfin_[set].as<uint64_t>(), W);
+  MSM_HIP_CHECK(hipGetLastError());
+}
+
+template <int G>
+void WeightedReducer<G>::copy_out_group_bits(hipStream_t s, int set, int nmsm, void *host) {
+  MSM_HIP_CHECK(hipMemcpyAsync(host, bgfin_[set].p, (size_t)nmsm * bit_bytes(), hipMemcpyDefault, s));
+}
+
+// window 0's sum_b b S_b from its 2 s bit sums (bit j of the weight: low half
+// block j < s, high half s + j): Horner from the top bit, as read_windows
+template <int G>
+hfp::Jac<typename HostField<G>::F> WeightedReducer<G>::combine_bits(const void *host) const {
+  const hfp::Jac<HF> *B = reinterpret_cast<const hfp::Jac<HF> *>(host);
+  const hfp::Jac<HF> *lo = B, *hi = B + sbits_;
+  hfp::Jac<HF> acc = hi[sbits_ - 1];
+  for (int j = 2 * sbits_ - 2; j >= 0; --j) {
+    acc = hfp::dbl(acc);
+    acc = hfp::addj(acc, j >= sbits_ ? hi[j - sbits_] : lo[j]);
+  }
+  return acc;
 }
 
 template <int G>
@@ -601,6 +682,7 @@ Ches<G>::~Ches() {
     if (tails_[t]) (void)hipStreamDestroy(tails_[t]);
   }
   if (host_out_) (void)hipHostFree(host_out_);
+  if (host_bits_) (void)hipHostFree(host_bits_);
   if (fstream_) (void)hipStreamDestroy(fstream_);
   if (cstream_) (void)hipStreamDestroy(cstream_);
 }
@@ -1015,6 +1097,37 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
   // caller's device exchange buffer (dev_out: ChesMulti gathers it over RCCL
   // and combines on the host; the combine below is then skipped)
   uint8_t *const out_base = dev_out ? static_cast<uint8_t *>(dev_out) : static_cast<uint8_t *>(host_out_);
+  // The batch's LAST reduction group ends in bit sums (launch_tail_group_bits):
+  // its tail runs after the last accumulation with the chip otherwise idle, and
+  // the bit phase is ~10 latency-bound levels instead of the dense stage's 2 s
+  // (profiles/r06_small_trace.txt).  Earlier groups keep the dense stage: their
+  // tails run beside accumulations, where the 2 s-Jacobian read-backs cost
+  // (DESIGN 5).  MSM_BIT_TAIL=0: dense stage for every group.
+  static const bool bit_tail_env = [] {
+    const char *e = getenv("MSM_BIT_TAIL");
+    return !e || atoi(e) != 0;
+  }();
+  const bool bit_tail = bit_tail_env && !dev_out && red.has_bit_tail();
+  const size_t bb = red.bit_bytes();
+  if (bit_tail && host_bits_bytes_ < (size_t)group_max * bb) {
+    if (host_bits_) (void)hipHostFree(host_bits_);
+    host_bits_ = nullptr;
+    host_bits_bytes_ = 0;
+    const size_t bytes = (size_t)std::max<size_t>(group_max, 32) * bb;
+    MSM_HIP_CHECK(hipHostMalloc(&host_bits_, bytes, hipHostMallocDefault));
+    host_bits_bytes_ = bytes;
+  }
+  // a group's tail + read-back: the dense stage into the read-back slots, or
+  // (the last group, bit_tail) the bit phase into host_bits_
+  auto group_tail = [&](hipStream_t ts, int rset, size_t first, size_t nmsm, bool last_group) {
+    if (bit_tail && last_group) {
+      red.launch_tail_group_bits(ts, rset, (int)nmsm, tail_coop);
+      red.copy_out_group_bits(ts, rset, (int)nmsm, host_bits_);
+    } else {
+      red.launch_tail_group(ts, rset, (int)nmsm, tail_coop && last_group);
+      red.copy_out_group(ts, rset, (int)nmsm, out_base + first * ob);
+    }
+  };
   // (group size cap: kFrontGroupDefault, or MSM_FRONT_GROUP=<1..8>; engine.hpp)
   // (small MSMs on lanes: groups of 2 on two lanes -- half the front launches,
   // measured 0.551 -> 0.530 ms per 2^17 MSM and 0.874 -> 0.845 at 2^18 -- and 4
@@ -1321,8 +1434,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
         const size_t q = grp(k), first = gfirst[q];
         MSM_HIP_CHECK(hipStreamWaitEvent(ts, evh[k], 0));  // this lane's level 0s of group q
         if (k0 >= 1 && k0 - 1 >= first) MSM_HIP_CHECK(hipStreamWaitEvent(ts, evh[k0 - 1], 0));  // the other lane's
-        red.launch_tail_group(ts, (int)(q % nred), (int)(k - first + 1), tail_coop && k + 1 == count);
-        red.copy_out_group(ts, (int)(q % nred), (int)(k - first + 1), out_base + first * ob);
+        group_tail(ts, (int)(q % nred), first, k - first + 1, k + 1 == count);
         MSM_HIP_CHECK(hipEventRecord(evt[q], ts));
       }
       issue_fronts(g + nfr - 1);
@@ -1351,8 +1463,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
         MSM_HIP_CHECK(hipEventRecord(evh[k], L));
         if (gend(k)) {  // the group's level 0s are done on both lanes
           for (int d = 0; d < nl && d <= slot; ++d) MSM_HIP_CHECK(hipStreamWaitEvent(ts, evh[k - d], 0));
-          red.launch_tail_group(ts, gset, slot + 1, tail_coop && k + 1 == count);
-          red.copy_out_group(ts, gset, slot + 1, out_base + (k - slot) * ob);
+          group_tail(ts, gset, k - slot, slot + 1, k + 1 == count);
           MSM_HIP_CHECK(hipEventRecord(evt[q], ts));
         }
       }
@@ -1376,8 +1487,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
     if (!gend(p)) return;
     hipStream_t ts = tails_[pq % 2];
     MSM_HIP_CHECK(hipStreamWaitEvent(ts, evh[p], 0));
-    red.launch_tail_group(ts, (int)(pq % 2), (int)pslot + 1, tail_coop && p + 1 == count);
-    red.copy_out_group(ts, (int)(pq % 2), (int)pslot + 1, out_base + (p - pslot) * ob);
+    group_tail(ts, (int)(pq % 2), p - pslot, pslot + 1, p + 1 == count);
     MSM_HIP_CHECK(hipEventRecord(evt[pq], ts));
   };
   auto l0_set_free = [&](size_t p) {  // level 0 of MSM p may write its reducer set
@@ -1436,8 +1546,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
       red.launch_head_slot(ts, buckets_[bset].p, gset, slot);
       MSM_HIP_CHECK(hipEventRecord(evh[k], ts));
       if (gend(k)) {  // the reduction group's last MSM
-        red.launch_tail_group(ts, gset, slot + 1, tail_coop && k + 1 == count);
-        red.copy_out_group(ts, gset, slot + 1, out_base + (k - slot) * ob);
+        group_tail(ts, gset, k - slot, slot + 1, k + 1 == count);
       }
     }
     issue_fronts(g + nfr - 1);
@@ -1453,7 +1562,11 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
   MSM_HIP_CHECK(hipStreamSynchronize(fstream_));  // three lanes: the group read-backs ran on the front stream
   // the per-MSM host Horner (~20 us each) over the host worker threads: with
   // one reduction group per batch every combine runs after the last tail
-  auto combine_k = [&](size_t k) { outs[k] = red.combine((const uint8_t *)host_out_ + k * ob)[0]; };
+  const size_t last_first = gfirst[ngroups - 1];  // the last group's MSMs: host_bits_ when bit_tail
+  auto combine_k = [&](size_t k) {
+    outs[k] = bit_tail && k >= last_first ? red.combine_bits((const uint8_t *)host_bits_ + (k - last_first) * bb)
+                                          : red.combine((const uint8_t *)host_out_ + k * ob)[0];
+  };
   if (dev_out) {
     // the window sums stay in dev_out for the caller's exchange
   } else if (count >= 4) {

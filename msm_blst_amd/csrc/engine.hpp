@@ -203,6 +203,7 @@ class WeightedReducer {
   // their ScanReducer buffers), the bit-phase read-back (engine pool budget)
   size_t device_bytes() const {
     size_t b = idx_.bytes + bfin_.bytes;
+    for (int t = 0; t < NSETS; ++t) b += bgfin_[t].bytes;
     for (const DevBuf &d : starts_) b += d.bytes;
     for (const DevBuf &d : bstarts_) b += d.bytes;
     for (int t = 0; t < NSETS; ++t)
@@ -235,6 +236,14 @@ class WeightedReducer {
   // (shortest latency when nothing else runs, e.g. the last group of a batch)
   void launch_tail_group(hipStream_t s, int set, int nmsm, bool coop = false);
   void copy_out_group(hipStream_t s, int set, int nmsm, void *host);  // nmsm * out_bytes()
+  // the same group tail ending in 2 s bit sums per MSM instead of the dense
+  // stage (one-window plans with a segment phase: has_bit_tail()); the host
+  // gets nmsm * bit_bytes() and combine_bits(MSM j's bytes) = combine(...)[0]
+  bool has_bit_tail() const { return bits_ && nout_.size() >= 2; }
+  size_t bit_bytes() const { return bit_slots() * 144 * G; }
+  void launch_tail_group_bits(hipStream_t s, int set, int nmsm, bool coop = false);
+  void copy_out_group_bits(hipStream_t s, int set, int nmsm, void *host);
+  hfp::Jac<HF> combine_bits(const void *host) const;
 
  private:
   size_t dense_slots() const { return (size_t)2 * nwin_ << sbits_; }
@@ -256,6 +265,7 @@ class WeightedReducer {
   std::vector<DevBuf> bstarts_;
   std::vector<size_t> bnout_;
   DevBuf bfin_;
+  DevBuf bgfin_[NSETS];  // group bit tails: nmsm x 2 s finalized bit sums per set
 };
 
 // digit/sort outputs of one MSM (entries sorted by bucket + schedule); the
@@ -480,6 +490,8 @@ class Ches {
   hipEvent_t ev_tail_[kBSets] = {nullptr, nullptr};
   void *host_out_ = nullptr;
   size_t host_out_bytes_ = 0;
+  void *host_bits_ = nullptr;  // the last group's bit-tail read-back (WeightedReducer::launch_tail_group_bits)
+  size_t host_bits_bytes_ = 0;
   std::vector<hipEvent_t> bev_;     // batch dependency events, one per (MSM, stage)
   std::vector<hipEvent_t> acc_ev_;  // batch profiling: events around each accumulation
   // digits + sort of nsets scalar sets (set_stride bytes apart) into front set `set`

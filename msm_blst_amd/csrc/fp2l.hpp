@@ -7,9 +7,11 @@
 // c0, odd lane: c1), halving the registers per lane.  Products need the
 // partner's component, fetched with one DPP quad_perm move per limb, and every
 // lane runs the SAME instruction stream on lane-selected operands (v_cndmask),
-// so the pair never diverges:
-//   c0 = a0 b0 + a1 (8p - b1)        even lane: fp_mul2(a, b, a', 8p - b')
-//   c1 = a0 b1 + a1 b0               odd lane:  fp_mul2(a', b, a, b')
+// so the pair never diverges.  Round 6: the lane-dependent choice sits on the
+// b side only, so the a operands enter the product in place (own a first,
+// partner a' second) and one select per product is saved:
+//   c0 = a0 b0 + a1 (8p - b1)        even lane: fp_mul2(a, b,  a', 8p - b')
+//   c1 = a1 b0 + a0 b1               odd lane:  fp_mul2(a, b', a', b)
 // (the same single-reduction sums as f_mul(Fp2) in fp.hpp, so every column and
 // value bound of DESIGN 4a carries over unchanged; ' = partner component).
 // ec.hpp's xyzz formulas are generic over the field type and run unchanged on
@@ -47,28 +49,26 @@ MSM_FN void pair_sel(Fp &r, bool c, const Fp &a, const Fp &b) {  // r = c ? a : 
 // a b, a lazy (< 6p, limbs < 2^30), b lazy (normalized here) -> S
 MSM_FN void f_mul(Fp2L &r, const Fp2L &a, const Fp2L &b) {
   const bool odd = pair_odd();
-  Fp bn = b.c, pa, pb, nb, X, Z, W;
+  Fp bn = b.c, pa, pb, nb, Y1, Y2;
   fp_norm(bn);
   pair_swap(pa, a.c);
   pair_swap(pb, bn);
   fp_neg<8>(nb, pb);
-  pair_sel(X, odd, pa, a.c);
-  pair_sel(Z, odd, a.c, pa);
-  pair_sel(W, odd, pb, nb);
-  fp_mul2(r.c, X, bn, Z, W);
+  pair_sel(Y1, odd, pb, bn);  // even b, odd b'
+  pair_sel(Y2, odd, bn, nb);  // even 8p - b', odd b
+  fp_mul2(r.c, a.c, Y1, pa, Y2);
 }
 // b already normalized (class S)
 MSM_FN void f_mul_bs(Fp2L &r, const Fp2L &a, const Fp2L &b) {
   const bool odd = pair_odd();
-  Fp pa, pb, nb, X, Z, W;
+  Fp pa, pb, nb, Y1, Y2;
   pair_swap(pa, a.c);
   pair_swap(pb, b.c);
   fp_neg<8>(nb, pb);
-  pair_sel(X, odd, pa, a.c);
-  pair_sel(Z, odd, a.c, pa);
-  pair_sel(W, odd, pb, nb);
+  pair_sel(Y1, odd, pb, b.c);  // even b, odd b'
+  pair_sel(Y2, odd, b.c, nb);  // even 8p - b', odd b
   Fp t;
-  fp_mul2(t, X, b.c, Z, W);
+  fp_mul2(t, a.c, Y1, pa, Y2);
   r.c = t;
 }
 // (a0 + a1 i)^2: c0 = (a0 + a1)(a0 + 32p - a1), c1 = a0 (2 a1), inputs < 18p
@@ -108,27 +108,27 @@ MSM_FN bool f_is_zero_S(const Fp2L &a) {
 MSM_FN void f_mul3(Fp2L &r, const Fp2L &a) { f_mul3(r.c, a.c); }
 // a b - c d (a lazy, b lazy normalized here, c, d in S), as f_mul_sub(Fp2):
 //   r0 = a0 b0 + a1 (8p - b1) + c0 (8p - d0) + c1 d1
-//   r1 = a0 b1 + a1 b0 + c0 (8p - d1) + c1 (8p - d0)
+//   r1 = a1 b0 + a0 b1 + c1 (8p - d0) + c0 (8p - d1)
+// own operands first, partner second, the lane choice on the b / d side:
+//   even: a b + a' (8p - b') + c (8p - d) + c' d'
+//   odd:  a b' + a' b + c (8p - d') + c' (8p - d)
 MSM_FN void f_mul_sub(Fp2L &r, const Fp2L &a, const Fp2L &b, const Fp2L &c, const Fp2L &d) {
   const bool odd = pair_odd();
-  Fp bn = b.c, pa, pb, pc, pd, nd, npd, o1, o3, o4, o5, o7, o8;
+  Fp bn = b.c, pa, pb, pc, pd, nd, npb, Y1, Y2, Y3, Y4;
   fp_norm(bn);
   pair_swap(pa, a.c);
   pair_swap(pb, bn);
   pair_swap(pc, c.c);
   pair_swap(pd, d.c);
-  fp_neg<8>(nd, d.c);
-  fp_neg<8>(npd, pd);
-  pair_sel(o1, odd, pa, a.c);
-  pair_sel(o3, odd, a.c, pa);
-  Fp npb;
   fp_neg<8>(npb, pb);
-  pair_sel(o4, odd, pb, npb);
-  pair_sel(o5, odd, pc, c.c);
-  pair_sel(o7, odd, c.c, pc);
-  pair_sel(o8, odd, npd, pd);
+  fp_neg<8>(nd, d.c);
+  pair_sel(Y1, odd, pb, bn);   // even b, odd b'
+  pair_sel(Y2, odd, bn, npb);  // even 8p - b', odd b
+  pair_sel(Y3, odd, pd, d.c);  // even d, odd d' ...
+  fp_neg<8>(Y3, Y3);           // ... negated: 8p - d / 8p - d'
+  pair_sel(Y4, odd, nd, pd);   // even d', odd 8p - d
   Fp t;
-  fp_mul4(t, o1, bn, o3, o4, o5, nd, o7, o8);
+  fp_mul4(t, a.c, Y1, pa, Y2, c.c, Y3, pc, Y4);
   r.c = t;
 }
 

@@ -157,6 +157,23 @@ __device__ __forceinline__ void accumulate_pair(const AccSched &S, const PT *__r
   const PayloadStream ps(S, pos);
   Xyzz<Fp2L> acc;
   xyzz_set_inf(acc);
+#if MSM_ACC2P_PREFETCH
+  // the next entry's row is loaded before this entry's madd (28 VGPRs of the
+  // 256 a 2-wave kernel has), so its HBM latency hides behind the madd's issue
+  uint32_t e = cnt ? ps.at(0) : 0u;
+  Aff<Fp2L> nxt;
+  if (cnt) ld_point2l(nxt, &pts[e & 0x7fffffffu], comp);
+  for (uint32_t k = 0; k < cnt; ++k) {
+    const Aff<Fp2L> p = nxt;
+    const uint32_t ce = e;
+    if (k + 1 < cnt) {
+      e = ps.at(k + 1);
+      ld_point2l(nxt, &pts[e & 0x7fffffffu], comp);
+    }
+    if (f_is_zero_exact(p.x) && f_is_zero_exact(p.y)) continue;  // affine infinity (ec_ops.h:717)
+    xyzz_madd(acc, p, (ce >> 31) != 0);
+  }
+#else
   for (uint32_t k = 0; k < cnt; ++k) {
     const uint32_t e = ps.at(k);
     Aff<Fp2L> p;
@@ -164,10 +181,27 @@ __device__ __forceinline__ void accumulate_pair(const AccSched &S, const PT *__r
     if (f_is_zero_exact(p.x) && f_is_zero_exact(p.y)) continue;  // affine infinity (ec_ops.h:717)
     xyzz_madd(acc, p, (e >> 31) != 0);
   }
+#endif
   st_xyzz2l(&buckets[S.order[pos]], acc, comp);
 }
+// MSM_ACC2P_PREFETCH=1 (build-time A/B knob): the next entry's row is loaded
+// during the current madd (247 VGPRs, no scratch).  Measured equal, so the G2
+// accumulation is not row-latency-bound: configs[4] 168.2 / 167.5 vs 167.1 /
+// 166.8 M pairs/s, accumulation 5.71-5.72 vs 5.70 ms (profiles/r06_g2_prefetch_ab.txt)
+#ifndef MSM_ACC2P_PREFETCH
+#define MSM_ACC2P_PREFETCH 0
+#endif
+// waves per SIMD the G2 accumulation is compiled for (0: no occupancy bound)
+#ifndef MSM_ACC2P_WAVES
+#define MSM_ACC2P_WAVES 0
+#endif
+#if MSM_ACC2P_WAVES
+#define MSM_ACC2P_BOUNDS __launch_bounds__(256, MSM_ACC2P_WAVES)
+#else
+#define MSM_ACC2P_BOUNDS __launch_bounds__(256)
+#endif
 template <class PT>
-__global__ void __launch_bounds__(256)
+__global__ void MSM_ACC2P_BOUNDS
     k_accumulate2p(const AccSched S, const PT *__restrict__ pts, Xyzz<Fp2> *__restrict__ buckets, size_t nbuckets) {
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t < 2 * nbuckets) accumulate_pair(S, pts, buckets, t);  // whole pairs only: 2 nbuckets lanes
@@ -175,7 +209,7 @@ __global__ void __launch_bounds__(256)
 
 // k_accumulate_sets (kernels.hpp) for G2: R sets in one grid, lane pairs
 template <class PT>
-__global__ void __launch_bounds__(256)
+__global__ void MSM_ACC2P_BOUNDS
     k_accumulate2p_sets(const AccSched S, const AccStride st, const PT *__restrict__ pts, Xyzz<Fp2> *__restrict__ buckets,
                         size_t nbuckets) {
   const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;

@@ -40,10 +40,11 @@ def test_ches_config_per_group_and_shard_size():
     """The configuration each bench line uses: G1 2^20 the reference's
     config_file_n_exp_20.h, G2 2^20 its _beta variant (measured faster for G2,
     profiles/r05_g2_beta_ab.txt), the strong-scaling shards the reference's
-    file for their own point count, and an explicit --beta wins."""
+    file measured fastest for their point count, and an explicit --beta wins."""
     assert bench.ches_config(20) == (20, 0)
     assert bench.ches_config(20, group=2) == (20, 1)
-    for lg in (17, 18, 19):
+    assert bench.ches_config(17) == (17, 1)  # q = 2^19, measured faster for the 2^17 shard (r06_tail_ab.txt)
+    for lg in (18, 19):
         assert bench.ches_config(lg) == (lg, 0)
     assert bench.ches_config(20, 0, 2) == (20, 0)
     assert bench.ches_config(20, 1, 1) == (20, 1)
