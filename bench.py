@@ -50,12 +50,12 @@ METRIC = "G1 MSM point-scalar pairs/sec at n=2^20, 1/2/4/8 MI355X; bit-exact vs 
 METRIC_G2 = "G2 MSM point-scalar pairs/sec at n=2^20 (BASELINE configs[4]); bit-exact vs CPU"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 MADS_PER_FPMUL = 392           # 14x14 product + 14x14 reduction, one v_mad_u64_u32 each (fp.hpp)
-FPMUL_PEAK = 76.8e9            # round-2 register-resident Fp-mul/s (profiles/r02_fp_rate.txt): fallback only, the
+FPMUL_PEAK = 76.8e9            # round-2 register-resident Fp-mul/s (profiles/archive_r01_r04.txt (r02_fp_rate.txt)): fallback only, the
                                # line prices against msm_valu_probe's rates measured in the same run
 MADD_RATE_R02 = 7.32e9         # round-2 register-resident G1 xyzz madd/s: fallback only
 AFFINE_BYTES = 96              # one G1 affine point (blst layout), SURVEY 8d
 FPMUL_PER_MADD = 10            # 8M + 2S (ec_ops.h:727-748)
-MAD_RATE = 30.36e12            # round-2 chip v_mad_u64_u32 rate (profiles/r02_instr_rate.txt): fallback only
+MAD_RATE = 30.36e12            # round-2 chip v_mad_u64_u32 rate (profiles/archive_r01_r04.txt (r02_instr_rate.txt)): fallback only
 CPU_THREADS = 16               # the GPU box's CPU share per GPU (16 threads)
 CPU_SETS = 3                   # scalar sets in the 1-thread CPU sample (~12 s at 2^20)
 # (group, log_n) -> the ches_config_files variant used by default: G1 2^20 keeps config_file_n_exp_20.h
@@ -80,7 +80,7 @@ def ches_config(log_n, beta=None, group=1):
     return log_n, DEFAULT_BETA.get((group, log_n), 0)
 
 
-def isa_mads_per_madd(G=1, path=os.path.join(REPO, "profiles", "r04_isa_counts.txt")):
+def isa_mads_per_madd(G=1, path=os.path.join(REPO, "profiles", "r06_isa_counts.txt")):
     """v_mad_u64_u32 per xyzz madd on its main path, from the gfx950 ISA of the
     shipped field code (tools/isa_report.sh): the madd is 6 products (U2, S2,
     PPP, Q, ZZ3, ZZZ3), 2 squares (PP, R^2) and one fused two-product sum
@@ -95,7 +95,7 @@ def isa_mads_per_madd(G=1, path=os.path.join(REPO, "profiles", "r04_isa_counts.t
                for k in keys]
         return (6 * cnt[0] + 2 * cnt[1] + cnt[2]) * (1 if G == 1 else 2), os.path.basename(path)
     except Exception:
-        return (3567, "profiles/r03_isa_counts.txt (constant)") if G == 1 else (None, "no lane-pair counts")
+        return (3567, "profiles/archive_r01_r04.txt (r03_isa_counts.txt) (constant)") if G == 1 else (None, "no lane-pair counts")
 
 
 def log(*a):
@@ -205,7 +205,7 @@ def main():
     ap.add_argument("--setup-batch", type=int, choices=(0, 1), default=0,
                     help="study knob: the context's setup ends with one untimed pipelined batch over the K resident "
                          "sets, before the W warm-up steps (measured no effect on the first timed batch, "
-                         "profiles/r04_setup_batch_ab.txt)")
+                         "profiles/archive_r01_r04.txt (r04_setup_batch_ab.txt))")
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the other BASELINE configs' legs (configs[0], [1], [4], the blst drop-in at 2^20)")
     ap.add_argument("--no-shards", action="store_true",

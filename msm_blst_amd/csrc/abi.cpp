@@ -34,7 +34,7 @@ int fail(int code, const std::string &msg) {
 }
 
 // window of the blst drop-in's plain Pippenger: the fastest c measured on
-// MI355X per n (tools/window_sweep.py, profiles/r03_window_sweep.json; blst's
+// MI355X per n (tools/window_sweep.py, profiles/archive_r01_r04.txt (r03_window_sweep.json); blst's
 // own rule, multi_scalar.c:268-275, picks smaller windows: CPU buckets are
 // cache-bound, GPU lanes want enough buckets to fill the chip)
 int auto_window(size_t n) {

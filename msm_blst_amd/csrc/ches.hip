@@ -260,7 +260,7 @@ void WeightedReducer<G>::plan(const std::vector<uint32_t> &w, const std::vector<
   // lane.  Large plans keep 8 (few lanes per item, fewest levels); small ones
   // (a few hundred thousand items: plain Pippenger at 2^16, CHES shards of
   // 2^17..2^19) would leave the chip < 1 wave per SIMD deep with 7-add chains
-  // (the 2^16 level 0 ran 103 us for 311 K adds, profiles/r04_fixed_cost.txt),
+  // (the 2^16 level 0 ran 103 us for 311 K adds, profiles/archive_r01_r04.txt (r04_fixed_cost.txt)),
   // so they take 4 or 2 and one or two more (tail) levels.  The adds are the
   // same in total (items - segments); MSM_L0_CHUNK=<2..64> overrides.
   static const int C0env = [] {
@@ -729,7 +729,7 @@ int Ches<G>::batch_lanes() const {
   if (env) return env;
   // G1 small MSMs take three lanes since round 4's single reduction group per
   // batch (2^17 / 2^18 / 2^19 batches 0.52 / 0.86 / 1.40 -> 0.49 / 0.80 / 1.35
-  // ms per MSM, profiles/r04_small_lanes_ab.txt); G2 keeps two (not measured)
+  // ms per MSM, profiles/archive_r01_r04.txt (r04_small_lanes_ab.txt)); G2 keeps two (not measured)
   const size_t lanes = bucket_count() * (G == 2 ? 2 : 1);
   return lanes < (size_t)3 * (G == 2 ? 2 : 3) * 1024 * 64 ? (G == 1 ? 3 : 2) : 1;
 }
@@ -1131,7 +1131,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
   // (group size cap: kFrontGroupDefault, or MSM_FRONT_GROUP=<1..8>; engine.hpp)
   // (small MSMs on lanes: groups of 2 on two lanes -- half the front launches,
   // measured 0.551 -> 0.530 ms per 2^17 MSM and 0.874 -> 0.845 at 2^18 -- and 4
-  // on three lanes (profiles/r04_small_lanes_ab.txt); the 2^20 batch keeps 1,
+  // on three lanes (profiles/archive_r01_r04.txt (r04_small_lanes_ab.txt)); the 2^20 batch keeps 1,
   // its wider fronts starve the accumulation, r03_front_group_ab.txt and
   // r04_front_group_ab.txt)
   static const size_t fg_env = [] {
@@ -1142,7 +1142,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
   // the batch fronts' fine-pass workgroup (bucket_sort.hpp k_bs_fine): 1024
   // threads; MSM_FINE_BT=256 selects the variant that fits beside three
   // accumulation waves per SIMD -- measured slower (H2D 408-411 vs 415-420 M,
-  // resident 423-429 vs 434-440 M pairs/s, profiles/r04_fine_bt_ab.txt)
+  // resident 423-429 vs 434-440 M pairs/s, profiles/archive_r01_r04.txt (r04_fine_bt_ab.txt))
   static const int fine_bt = [] {
     const char *e = getenv("MSM_FINE_BT");
     return e && atoi(e) == 256 ? 256 : 1024;
@@ -1183,7 +1183,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
   // periods of a few hundred us) keeps fronts further ahead and lets group q
   // reuse reducer set q % 4 after tail q - 4 (a tail is ~30 latency-bound
   // launches, ~1 ms beside the accumulations: with 2 sets group q + 2 waited
-  // for it, profiles/r04_batch_trace_2p17.txt)
+  // for it, profiles/archive_r01_r04.txt (r04_batch_trace_2p17.txt))
   // Front phase (small-MSM accumulation groups; MSM_FRONT_PHASE=1 enables):
   // one front set per front group, up to kFrontPhase (capped at ~4 GiB of
   // front sets), and the first accumulation waits for every front of that
@@ -1218,7 +1218,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
   // (copies issued 4 MSMs ahead, each after a front event) the 2^20 H2D
   // headline fell into a slow schedule in about half the runs (372-391 vs
   // 411-417 M pairs/s, more often after a 3-set warm-up); with a slot per set
-  // every run gave 418-423 M (profiles/r04_h2d_slots_ab.txt)
+  // every run gave 418-423 M (profiles/archive_r01_r04.txt (r04_h2d_slots_ab.txt))
   static const size_t nsg_env = [] {
     const char *e = getenv("MSM_H2D_SLOTS");  // A/B knob: slot groups (copies issued that far ahead)
     return (size_t)(e ? std::max(2, std::min(256, atoi(e))) : 0);
@@ -1262,7 +1262,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
   //              accumulation, then, after the group's last MSM, ONE launch per
   //              tail level for the whole group and one read-back.  Every launch
   //              that runs beside an accumulation costs it ~10-20 us
-  //              (profiles/r02_batch_sched2.txt), so the ~35 latency-bound levels
+  //              (profiles/archive_r01_r04.txt (r02_batch_sched2.txt)), so the ~35 latency-bound levels
   //              are paid once per group, not once per MSM.  Two streams: group
   //              q+1's level 0s never queue behind group q's tail;
   //   cstream_:  host scalars: the H2D copies of front group g's sets into slot
@@ -1347,7 +1347,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
       MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, eva[last], 0));
       // A/B knob: also after that MSM's level 0, so the front starts beside the
       // next accumulation instead of beside level 0 (one-lane schedule);
-      // measured no better (profiles/r04_h2d_slots_ab.txt, call 19)
+      // measured no better (profiles/archive_r01_r04.txt (r04_h2d_slots_ab.txt), call 19)
       if (front_after_l0 && nl < 2) MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, evh[last], 0));
       for (size_t d = 1; d < (size_t)nl && last >= d && last - d >= fgb[g - nfr]; ++d)  // its other lanes
         MSM_HIP_CHECK(hipStreamWaitEvent(fstream_, eva[last - d], 0));
@@ -1364,8 +1364,8 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
   // ahead and every accumulation started at once beside the previous level 0:
   // level 0 then took 0.5-1.2 ms instead of 0.41, the accumulations 2.2-2.7 ms
   // instead of 1.8, and the H2D headline 342-386 M pairs/s instead of ~420
-  // (kernel traces, profiles/r03_spread_trace.txt); with it 19 of 19 runs on
-  // three boxes gave 410-422 M (profiles/r03_ab_studies.txt r03a0*).
+  // (kernel traces, profiles/archive_r01_r04.txt (r03_spread_trace.txt)); with it 19 of 19 runs on
+  // three boxes gave 410-422 M (profiles/archive_r01_r04.txt (r03_ab_studies.txt) r03a0*).
   // G2 (5-ms accumulations, 1.2-ms level 0) never showed the slow mode and
   // runs 1.5 % faster free-running (r03a0g2), so the wait is the G1 default;
   // MSM_ACC_AFTER_L0=0 / =1 forces either schedule for both groups.
@@ -1472,7 +1472,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
   }
   // Level 0 inside the next accumulation's grid (A/B knob, off by default:
   // measured slower, resident 434-438 vs 446-450 M pairs/s, G2 164.4 vs 165.3 M,
-  // profiles/r04_l0_fuse_ab.txt; MSM_L0_FUSE=1: level-0 workgroups first, =2:
+  // profiles/archive_r01_r04.txt (r04_l0_fuse_ab.txt); MSM_L0_FUSE=1: level-0 workgroups first, =2:
   // last; k_accumulate_l0 / k_accumulate2p_l0): MSM k's launch also runs
   // level 0 of MSM k - 1 on the caller's stream, the last MSM's level 0 runs
   // alone after the loop, and reducer set q % 2 is reused by group q + 2 only

@@ -460,7 +460,7 @@ class Ches {
   // batch: MSMs per reduction group (WeightedReducer::launch_tail_group).  20:
   // a batch of up to 20 runs one tail, after its last accumulation, instead of
   // tails beside accumulations (each costs the one beside it ~0.3 ms); 20 vs
-  // 8 measured +1.2 % (profiles/r04_red_group_ab.txt).  MSM_RED_GROUP overrides.
+  // 8 measured +1.2 % (profiles/archive_r01_r04.txt (r04_red_group_ab.txt)).  MSM_RED_GROUP overrides.
   static constexpr int kGroup = 20;
   static constexpr int kFrontGroup = 8;  // batch: largest front group (ramping up 1, 1, 2, 4, 8)
   static constexpr int kFrontGroupDefault = 1;
@@ -481,7 +481,7 @@ class Ches {
   // synchronous MSM's latency; in a batch level 0 runs beside other lanes'
   // accumulations while the grouped tail runs exposed after the last one, so
   // the batch moves the adds into level 0 (2^17: the group tail's first segment
-  // level alone was 0.51 ms, profiles/r04_batch_trace_2p17_lanes3.txt).
+  // level alone was 0.51 ms, profiles/archive_r01_r04.txt (r04_batch_trace_2p17_lanes3.txt)).
   // MSM_BATCH_L0_CHUNK=<2..64> overrides 8; =0 reuses red_.
   WeightedReducer<G> bred_;
   WeightedReducer<G> *batch_red_ = &red_;

@@ -1,6 +1,6 @@
 """CPU tests of bench.py's host-side accounting: the per-madd v_mad_u64_u32
 count behind `valu_roofline.mad_frac` is parsed from the committed gfx950 ISA
-counts (tools/isa_report.sh -> profiles/r04_isa_counts.txt) for G1 (Fp ops on
+counts (tools/isa_report.sh -> profiles/r06_isa_counts.txt) for G1 (Fp ops on
 one lane) and G2 (lane-pair Fp2 ops, both lanes)."""
 import os
 import re
@@ -11,7 +11,7 @@ sys.path.insert(0, REPO)
 
 import bench  # noqa: E402
 
-ISA = os.path.join(REPO, "profiles", "r04_isa_counts.txt")
+ISA = os.path.join(REPO, "profiles", "r06_isa_counts.txt")
 
 
 def _mads(txt, key):

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Batch-rate probe used for the schedule studies of DESIGN 5
-(profiles/r02_batch_sched2.txt): G1 CHES 2^20, K distinct scalar sets, resident
+(profiles/archive_r01_r04.txt (r02_batch_sched2.txt)): G1 CHES 2^20, K distinct scalar sets, resident
 and pinned-host batches, best of R runs, results checked equal across runs.
 usage: exp_batch.py [K] [R]"""
 import os
