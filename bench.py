@@ -819,7 +819,8 @@ def shard_legs(m, mdist, torch, dev, local, sp, host, K, W, headline_value):
         folded = mdist.fold(parts0, add)
         out[f"shard{N}"] = leg(proj, worst / K * 1e3, (m.compress(1, folded).hex() == want if want else None)
                                and all(eqs), eff=round(proj / (N * headline_value), 4),
-                               cfg=f"q{params['q_exp']}h{params['h']}")
+                               cfg=f"q{params['q_exp']}h{params['h']}",
+                               ms_all=[round(x / K * 1e3, 3) for x in times])
     return out
 
 
