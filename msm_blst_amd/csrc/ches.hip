@@ -1164,9 +1164,7 @@ void Ches<G>::run_jobs(hipStream_t s, const uint8_t *scalars, size_t stride, siz
   // groups accumulate: a set copies in ~0.6 ms, an MSM accumulates in ~2.3) are
   // in HBM before its front is due -- a first group of eight stalled the H2D
   // batch by ~5 ms (the 256-MiB copy, then the front, before MSM 1).
-  std::vector<size_t> fgb{0};
-  while (fgb.back() < count)
-    fgb.push_back(std::min(count, fgb.back() + std::min<size_t>(fg_max, std::max<size_t>(1, fgb.back()))));
+  const std::vector<size_t> fgb = front_groups(count, fg_max);
   const size_t nfg = fgb.size() - 1;
   // every buffer the loop touches exists before the first launch (an allocation
   // inside the issue loop could synchronise the device)

@@ -342,9 +342,7 @@ void Pippenger<G>::run_batch(hipStream_t s, const uint8_t *d_scalars, size_t str
     return (size_t)(e ? std::max(1, std::min(8, atoi(e))) : 4);
   }();
   const size_t fg_max = fg_env;
-  std::vector<size_t> fgb{0};
-  while (fgb.back() < count)
-    fgb.push_back(std::min(count, fgb.back() + std::min<size_t>(fg_max, std::max<size_t>(1, fgb.back()))));
+  const std::vector<size_t> fgb = front_groups(count, fg_max);
   const size_t nfg = fgb.size() - 1;
   const size_t ngroups = (count + group_max - 1) / group_max, R = (count + ngroups - 1) / ngroups;
   const size_t ob = red.out_bytes();

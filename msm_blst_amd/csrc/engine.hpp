@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -24,6 +25,34 @@ namespace msm {
 class HostStager;  // hoststage.hpp: pinned-ring uploads from pageable caller memory
 
 inline unsigned nblk(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b); }
+
+// Front groups of a batch (MSMs [fgb[g], fgb[g + 1]) share one digits + sort
+// pass and, for small MSMs, one accumulation launch): 1, 1, 2, 4, then fg_max
+// each.  taper (MSM_FRONT_TAPER=1, A/B knob): the last group split in halves
+// down to one MSM (4 -> 2, 1, 1), so the level 0 that follows the batch's last
+// accumulation covers one MSM and the earlier level 0s run beside the last
+// accumulations.
+inline std::vector<size_t> front_groups(size_t count, size_t fg_max) {
+  static const bool taper = [] {
+    const char *e = getenv("MSM_FRONT_TAPER");
+    return e && atoi(e) != 0;
+  }();
+  std::vector<size_t> fgb{0};
+  while (fgb.back() < count)
+    fgb.push_back(std::min(count, fgb.back() + std::min<size_t>(fg_max, std::max<size_t>(1, fgb.back()))));
+  if (taper && fgb.size() >= 2) {
+    size_t first = fgb[fgb.size() - 2], len = count - first;
+    fgb.pop_back();
+    while (len > 1) {
+      const size_t half = (len + 1) / 2;
+      fgb.push_back(first + half);
+      first += half;
+      len -= half;
+    }
+    fgb.push_back(count);
+  }
+  return fgb;
+}
 
 struct DevBuf {
   void *p = nullptr;

@@ -68,6 +68,21 @@ template <class F>
 __device__ __forceinline__ Aff<F> ld_point(const AffP<F> *p) {
   return ld16(reinterpret_cast<const Aff<F> *>(p));
 }
+// one coordinate (0: x, 1: y) of a G1 table row, 8-B loads
+__device__ __forceinline__ Fp ld_coord(const AffP<Fp> *p, int c) {
+  const uint2 *s = reinterpret_cast<const uint2 *>(reinterpret_cast<const uint8_t *>(p) + c * sizeof(Fp));
+  Fp r;
+#pragma unroll
+  for (int i = 0; i < NL / 2; ++i) {
+    const uint2 v = s[i];
+    r.v[2 * i] = v.x;
+    r.v[2 * i + 1] = v.y;
+  }
+  return r;
+}
+__device__ __forceinline__ Fp ld_coord(const Aff<Fp> *p, int c) {
+  return ld_coord(reinterpret_cast<const AffP<Fp> *>(p), c);
+}
 template <class F>
 __device__ __forceinline__ void st_point(Aff<F> *p, const Aff<F> &a) {
   st16(p, a);
@@ -258,6 +273,9 @@ static __global__ void k_iota(uint32_t *a, size_t n) {
   if (i < n) a[i] = (uint32_t)i;
 }
 
+#ifndef MSM_ACC_PREFETCH
+#define MSM_ACC_PREFETCH 0
+#endif
 // waves per SIMD the G1 accumulation is compiled for (VGPR budget 512 / waves)
 #ifndef MSM_ACC_WAVES
 #define MSM_ACC_WAVES 3
@@ -293,12 +311,48 @@ __device__ __forceinline__ void accumulate_bucket(const AccSched &S, const PT *_
   const PayloadStream ps(S, (uint32_t)t);
   Xyzz<F> acc;
   xyzz_set_inf(acc);
+#if MSM_ACC_PREFETCH == 2
+  // A/B knob (build time): the next entry's x loaded before this entry's madd,
+  // this entry's y at the top of its iteration (first used by the madd's second
+  // product); x == 0 exactly is the only way into the infinity test
+  uint32_t e = cnt ? ps.at(0) : 0u;
+  F nx;
+  if (cnt) nx = ld_coord(&pts[e & 0x7fffffffu], 0);
+  for (uint32_t k = 0; k < cnt; ++k) {
+    Aff<F> p;
+    p.x = nx;
+    const uint32_t ce = e;
+    p.y = ld_coord(&pts[ce & 0x7fffffffu], 1);
+    if (k + 1 < cnt) {
+      e = ps.at(k + 1);
+      nx = ld_coord(&pts[e & 0x7fffffffu], 0);
+    }
+    if (f_is_zero_exact(p.x) && f_is_zero_exact(p.y)) continue;  // affine infinity (ec_ops.h:717)
+    xyzz_madd(acc, p, (ce >> 31) != 0);
+  }
+#elif MSM_ACC_PREFETCH
+  // A/B knob (build time): the next entry's row loaded before this entry's madd
+  uint32_t e = cnt ? ps.at(0) : 0u;
+  Aff<F> nxt;
+  if (cnt) nxt = ld_point(&pts[e & 0x7fffffffu]);
+  for (uint32_t k = 0; k < cnt; ++k) {
+    const Aff<F> p = nxt;
+    const uint32_t ce = e;
+    if (k + 1 < cnt) {
+      e = ps.at(k + 1);
+      nxt = ld_point(&pts[e & 0x7fffffffu]);
+    }
+    if (f_is_zero_exact(p.x) && f_is_zero_exact(p.y)) continue;  // affine infinity (ec_ops.h:717)
+    xyzz_madd(acc, p, (ce >> 31) != 0);
+  }
+#else
   for (uint32_t k = 0; k < cnt; ++k) {
     const uint32_t e = ps.at(k);
     Aff<F> p = ld_point(&pts[e & 0x7fffffffu]);
     if (f_is_zero_exact(p.x) && f_is_zero_exact(p.y)) continue;  // affine infinity (ec_ops.h:717)
     xyzz_madd(acc, p, (e >> 31) != 0);
   }
+#endif
   st16(&buckets[S.order[t]], acc);
 }
 template <int G, class PT = Aff<typename FieldOf<G>::F>>
