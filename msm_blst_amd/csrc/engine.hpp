@@ -31,7 +31,8 @@ inline unsigned nblk(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b);
 // each.  taper (MSM_FRONT_TAPER=1, A/B knob): the last group split in halves
 // down to one MSM (4 -> 2, 1, 1), so the level 0 that follows the batch's last
 // accumulation covers one MSM and the earlier level 0s run beside the last
-// accumulations.
+// accumulations.  Measured no better (2^17 shard 0.429 / 0.411 vs 0.414 / 0.436
+// ms, configs[1] 0.340 / 0.341 vs 0.334 / 0.339; profiles/r06_taper_prefetch_ab.txt).
 inline std::vector<size_t> front_groups(size_t count, size_t fg_max) {
   static const bool taper = [] {
     const char *e = getenv("MSM_FRONT_TAPER");

@@ -273,6 +273,10 @@ static __global__ void k_iota(uint32_t *a, size_t n) {
   if (i < n) a[i] = (uint32_t)i;
 }
 
+// MSM_ACC_PREFETCH (build-time A/B knob): 1 loads the next entry's row during
+// the current madd (168 VGPRs + 44 B scratch, not run), 2 only its x (162
+// VGPRs): 2 measured slower in the batch (accumulation 1.81 vs 1.78 ms, H2D
+// headline 420-429 vs 432-433 M pairs/s; profiles/r06_taper_prefetch_ab.txt)
 #ifndef MSM_ACC_PREFETCH
 #define MSM_ACC_PREFETCH 0
 #endif
