@@ -27,6 +27,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CHILD = r"""
 import json, sys
 sys.path.insert(0, sys.argv[1])
+import numpy as np, torch
+torch.cuda.init()  # torch's HIP runtime first (tests/conftest.py _torch_hip_first)
 import msm_blst_amd as m
 out = {}
 for group, n_exp, K in ((1, 16, 25), (2, 10, 23)):
@@ -42,7 +44,6 @@ n, K = 1 << 12, 21
 pc = m.MSMContext(1, 0, 12)
 pc.set_points(m.fixed_points(1, n), n)
 raw = b"".join(bytes(m.gen_scalars(n, 1 if k == 0 else 400 + k)) for k in range(K))
-import numpy as np, torch
 d = torch.tensor(np.frombuffer(raw, dtype=np.uint8), device="cuda:0")
 got = [m.compress(1, r).hex() for r in pc.mult_batch(d.data_ptr(), K, 255, on_device=True)]
 sync = [m.compress(1, pc.mult(d.data_ptr() + 32 * n * k, 255, on_device=True)).hex() for k in (0, K - 1)]
