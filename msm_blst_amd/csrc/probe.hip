@@ -3,8 +3,8 @@
 // the round-2 constants of tools/microbench/fp_rate.hip were measured on
 // another box, and boxes differ by up to 12 % in the clock they hold).
 //
-//   k_probe_mad    8 independent v_mad_u64_u32 chains per lane: the chip's
-//                  integer mad issue rate (lane-ops/s)
+//   k_probe_mad    16 independent v_mad_u64_u32 chains per lane, 1-4 waves
+//                  per SIMD: the chip's integer mad issue rate (lane-ops/s)
 //   k_probe_fpmul  two independent register-resident Fp products per lane
 //                  (fp.hpp fp_mul, 392 mads each): Fp-mul/s
 //   k_probe_madd   G1 xyzz madd chains (ec.hpp xyzz_madd, the accumulation's
@@ -26,18 +26,18 @@ namespace {
 
 __global__ void __launch_bounds__(256) k_probe_mad(uint64_t *out, uint32_t seed, int iters) {
   const uint32_t t = threadIdx.x + blockIdx.x * blockDim.x;
-  uint64_t acc[8];
+  uint64_t acc[16];
   const uint32_t a = t | 1, b = seed | 3;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) acc[k] = t + k;
+  for (int k = 0; k < 16; ++k) acc[k] = t + k;
   for (int it = 0; it < iters; ++it) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
+    for (int k = 0; k < 16; ++k)
       asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(acc[k]) : "v"(a), "v"(b) : "vcc");
   }
   uint64_t s = 0;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) s += acc[k];
+  for (int k = 0; k < 16; ++k) s += acc[k];
   if (s == 0x123456789ull) out[t] = s;  // never true in practice; keeps the chains live
 }
 
@@ -124,13 +124,13 @@ void valu_probe(int device, double out[4]) {
     MSM_HIP_CHECK(hipMemcpy(pbuf.p, h, sizeof(h), hipMemcpyHostToDevice));
     double mad = 0, fpm = 0, madd = 0;
     float total = 0;
-    for (int bpc : {4, 8}) {  // 256-thread blocks per CU = waves per SIMD
-      const int blocks = cus * bpc, iters = 4096;
+    for (int bpc : {4, 8, 16}) {  // 256-thread blocks per CU = waves per SIMD
+      const int blocks = cus * bpc, iters = 16384 / bpc;
       const float ms = best_ms([&] {
         hipLaunchKernelGGL(k_probe_mad, dim3(blocks), dim3(256), 0, 0, obuf.as<uint64_t>(), 7u, iters);
       });
       total += 4 * ms;
-      mad = std::max(mad, (double)blocks * 256 * iters * 8 / (ms * 1e-3));
+      mad = std::max(mad, (double)blocks * 256 * iters * 16 / (ms * 1e-3));
     }
     for (int bpc : {3, 4, 8}) {
       const int blocks = cus * bpc, iters = 256;
