@@ -292,6 +292,7 @@ void Pippenger<G>::run(hipStream_t s, const uint8_t *d_scalars, size_t stride, i
     *out = hfp::Jac<HF>{hfp::fzero(HF()), hfp::fzero(HF()), hfp::fzero(HF())};
     return;
   }
+  fs_[0].sort.fine_bt = 1024;  // alone on the chip: the 1024-thread fine pass
   front(s, d_scalars, stride, nbits, nullptr, fs_[0]);
   back(s, nbits, out);
 }
@@ -370,6 +371,13 @@ void Pippenger<G>::run_batch(hipStream_t s, const uint8_t *d_scalars, size_t str
   const int nfr = phase_env ? (int)std::max<size_t>(kFronts, std::min<size_t>(kFrontPhase, ((size_t)4 << 30) / fs_bytes))
                             : kFronts;
   if ((int)fs_.size() < nfr) fs_.resize(nfr);
+  // the batch fronts' fine-pass workgroup (bucket_sort.hpp k_bs_fine): 1024
+  // threads, or MSM_PIP_FINE_BT=256 (fits beside the accumulation waves)
+  static const int fine_bt = [] {
+    const char *e = getenv("MSM_PIP_FINE_BT");
+    return e && atoi(e) == 256 ? 256 : 1024;
+  }();
+  for (ChesFrontSet &f : fs_) f.sort.fine_bt = fine_bt;
   for (DevBuf &b : gbuckets_) b.ensure(fg_max * NT * sizeof(Xyzz<F>));
   for (int t = 0; t < kRedSets; ++t) red.ensure_group(t, (int)group_max);
   for (int f = 0; f < nfr; ++f)
@@ -484,6 +492,7 @@ void Pippenger<G>::run_host(hipStream_t s, const void *pts_blst, size_t n, const
   const size_t sbytes = n * stride;
   scal_.ensure(sbytes + (tile ? n * 5 : 0) + 16);
   stage_->upload(scal_.p, scalars, sbytes, s);
+  fs_[0].sort.fine_bt = 1024;  // a batch may have left its setting
   if (tile) {
     uint32_t *mag = reinterpret_cast<uint32_t *>(scal_.as<uint8_t>() + ((sbytes + 3) & ~(size_t)3));
     uint8_t *neg = reinterpret_cast<uint8_t *>(mag + n);
