@@ -77,3 +77,40 @@ def test_bit_tail_and_dense_coop_choices_agree(golden):
             assert r[key]["sync_ok"], key
             assert r[key]["got"][0] == w, key
             assert r[key]["got"] == runs[0][key]["got"], key
+
+
+@pytest.mark.parametrize("group,n_exp", [(1, 12), (2, 10)])
+def test_short_batches_equal_sync(group, n_exp):
+    """Batches of 1, 2 and 3 sets: a single reduction group that is also the
+    last (bit tail over one to three MSMs), the first front groups of the ramp
+    (1, 1, 2, ...) and, for K = 1, no second lane -- each result equal to the
+    synchronous MSM of its set."""
+    import msm_blst_amd as m
+    n = 1 << n_exp
+    ctx = m.CHESContext(group, 0, n_exp=n_exp)
+    ctx.build_table(m.fixed_points(group, n), n)
+    try:
+        for K in (1, 2, 3, 1):
+            sets = [bytes(m.gen_scalars(n, 500 + 10 * K + k)) for k in range(K)]
+            got = [m.compress(group, r) for r in ctx.mult_batch(b"".join(sets), K)]
+            want = [m.compress(group, ctx.mult(s)) for s in sets]
+            assert got == want, K
+    finally:
+        ctx.close()
+
+
+def test_short_plain_batches_equal_sync():
+    """configs[1]'s plain-Pippenger batch with 1, 2 and 3 sets (one reduction
+    group, dense tail) against the synchronous MSMs."""
+    import msm_blst_amd as m
+    n = 1 << 12
+    ctx = m.MSMContext(1, 0, 12)
+    ctx.set_points(m.fixed_points(1, n), n)
+    try:
+        for K in (1, 2, 3):
+            raw = b"".join(bytes(m.gen_scalars(n, 600 + 10 * K + k)) for k in range(K))
+            got = [m.compress(1, r) for r in ctx.mult_batch(raw, K, 255)]
+            want = [m.compress(1, ctx.mult(raw[32 * n * k:32 * n * (k + 1)], 255)) for k in range(K)]
+            assert got == want, K
+    finally:
+        ctx.close()
