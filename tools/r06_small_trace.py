@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Kernel-trace workload for the small-MSM batches (round 6): configs[1]'s
 plain-Pippenger batch (2^16, c = 14, K = 20 resident sets) and the 2^17 CHES
-shard batch of `bench.py --gpus 8` (config_file_n_exp_17.h, K = 20 pinned host
-sets), each after one untimed batch, separated by 50-ms host sleeps so
+shard batch of `bench.py --gpus 8` (bench.ches_config(17): config_file_n_exp_17_beta.h
+since round 6, K = 20 pinned host sets), each after one untimed batch, separated by 50-ms host sleeps so
 tools/batch_profile.py can split the trace into segments.
 usage: rocprofv3 --kernel-trace --output-format csv -d D -o run -- python3 tools/r06_small_trace.py
 """
@@ -34,7 +34,9 @@ for case in cases:
         host = torch.empty(K * n * 32, dtype=torch.uint8, pin_memory=True)
         for k in range(K):
             host.numpy()[k * n * 32:(k + 1) * n * 32] = np.frombuffer(m.gen_scalars(n, 1 + k), dtype=np.uint8)
-        ctx = m.CHESContext(1, 0, n_exp=17)
+        import bench  # noqa: E402
+        ne, beta = bench.ches_config(17)
+        ctx = m.CHESContext(1, 0, n_exp=ne, beta=beta)
         ctx.build_table(m.fixed_points(1, n), n, stream=sp)
         run = lambda: ctx.mult_batch(host.data_ptr(), K, 32, set_stride=n * 32, on_device=False, stream=sp)  # noqa: E731
     run()
