@@ -1,6 +1,7 @@
 #!/bin/bash
 # Same-box A/B of the last accumulation group's level 0 on two lanes per chunk
 # (MSM_L0_SPLIT, ches.hip run_jobs / pair_kernels.hpp k_segsum_split2) on the
+# (The k_segsum_split2 code measured equal and was removed; profiles/r06_l0_split_ab.txt.)
 # 2^17 / 2^18 CHES shard batches (tools/shard_leg_probe.py), after the batch
 # tail tests; two rounds alternating.  usage (via gpurun): bash tools/r06_ab_l0_split.sh
 set -o pipefail
