@@ -52,3 +52,18 @@ def test_rehearsal_lines_are_strong_scaling_with_parity():
         assert d["config"]["n_total"] == 1 << 20
         assert d["parity_vs_reference"] is True
         assert len(raw) < 7000
+
+
+def test_g2_line_shape():
+    """configs[4]'s line (bench.py --group 2): its own metric name, the G2
+    roofline priced on the probe's mad rate, parity, under 7 KB."""
+    raw = _last_line(os.path.join(REPO, "profiles", "r06_bench_g2.json"))
+    assert len(raw) < 7000
+    d = json.loads(raw)
+    for k in CONTRACT:
+        assert k in d, k
+    assert "G2" in d["metric"] and d["parity_vs_reference"] is True
+    r = d["roofline"]
+    assert r["valu_unit"] == "T mad/s" and 0 < r["valu_frac"] <= 1 and r["peak_basis"].startswith("this run")
+    for name, leg in d["legs"].items():
+        assert leg.get("ok", True) is True, name
