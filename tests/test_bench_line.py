@@ -67,3 +67,22 @@ def test_g2_line_shape():
     assert r["valu_unit"] == "T mad/s" and 0 < r["valu_frac"] <= 1 and r["peak_basis"].startswith("this run")
     for name, leg in d["legs"].items():
         assert leg.get("ok", True) is True, name
+
+
+def test_profiles_agree_with_the_line():
+    """The committed evidence behind the N = 1 line's roofline (final
+    session): the rocprofv3 kernel stats list the dominant kernel, the HIP-event
+    kernel time agrees with rocprof's average over the same timed launches
+    (roofline_check.json), and the line's `traffic` is the PMC pass's bytes per
+    launch (pmc_traffic.json, which bench.py reads)."""
+    prof = os.path.join(REPO, "profiles")
+    d = json.loads(_last_line(os.path.join(prof, "r06_bench.json")))
+    stats = open(os.path.join(prof, "r06_kernel_stats.csv")).read()
+    assert "k_accumulate<1" in stats
+    chk = json.load(open(os.path.join(prof, "r06_roofline_check.json")))
+    assert 0.95 < chk["rocprof_vs_bench"] < 1.05 and chk["timed_launches"] == d["steps"]
+    assert chk["scratch"] == "0"
+    pmc = json.load(open(os.path.join(prof, "r06_pmc_traffic.json")))
+    assert pmc == json.load(open(os.path.join(prof, "pmc_traffic.json")))
+    assert abs(pmc["accumulate_bytes_per_launch"] - d["roofline"]["traffic"]) / pmc["accumulate_bytes_per_launch"] < 1e-3
+    assert d["roofline"]["traffic"] > d["roofline"]["algorithmic_bytes_per_launch"]  # 128-B lines of 112-B rows
